@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mpixels/sec segmented at 4096x4096 RGB (BASELINE.json metric, config 3).
+
+One step = PictureService.watershed (PictureService.java:908-911) on one 4096x4096 synthetic
+mosaic frame already resident in HBM: the exact cv::watershed flood (labels written to a separate
+int32 buffer, the input markers stay pristine) + colorByIndexes(colored=false) into a BGR frame,
+through libmsegment's device entry point msg_watershed_colorize_dev.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N > 1 (launched by torch.distributed.run, one rank per GPU): every rank segments its own frame
+(BASELINE config 5: batched frames, one per GPU, no collectives -- weak scaling).  The only
+collectives are the timing barriers and the max-over-ranks of the elapsed time.
+
+Rank 0 prints ONE JSON line.  Extra objects: "roofline" (dominant kernel, HIP-event timed on the
+launch stream), "cpu_baseline" (the C oracle = same algorithm, timed on this host, rank 0, N=1).
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "opencv-msegment_amd"))
+
+METRIC = "Mpixels/sec segmented at 4096x4096 RGB; achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+# Algorithmic bytes (DESIGN.md "Kernels"): what each kernel must move at minimum per unit.
+BYTES_PER_PIXEL = {"k_prep": 13.0, "k_colorize": 7.0, "k_edge_weights": 5.0}
+BYTES_PER_ITEM = {"k_resolve": 40.0}        # per batch item resolved
+BYTES_SCATTER = (24.0, 12.0)                # per committed item, per appended push
+E2E_BYTES_PER_PIXEL = 14.0                  # 3 B BGR + 4 B markers in, 4 B labels + 3 B BGR out
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def timed_steps(step, steps, barrier, sync):
+    """Barrier + sync on both sides of exactly `steps` steps; returns this rank's seconds."""
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier()
+    return time.perf_counter() - t0
+
+
+def reduce_max(x, device=None):
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def kernel_roofline(prof, stats_per_step, npx, steps):
+    """Pick the kernel with the largest total time; achieved = algorithmic bytes per launch /
+    average launch duration (both from the same HIP-event-timed steps)."""
+    rows = []
+    for name, (launches, total_ms) in prof.items():
+        if launches == 0:
+            continue
+        if name in BYTES_PER_PIXEL:
+            alg = BYTES_PER_PIXEL[name] * npx * steps
+        elif name in BYTES_PER_ITEM:
+            alg = BYTES_PER_ITEM[name] * stats_per_step["items"] * steps
+        elif name == "k_scatter":
+            alg = (BYTES_SCATTER[0] * stats_per_step["pops"] + BYTES_SCATTER[1] * stats_per_step["pushes"]) * steps
+        else:
+            alg = None
+        avg_us = 1000.0 * total_ms / launches
+        gbs = (alg / launches) / (avg_us * 1e-6) / 1e9 if alg else None
+        rows.append({"kernel": name, "launches_per_step": launches / steps, "avg_us": round(avg_us, 3),
+                     "total_ms_per_step": round(total_ms / steps, 4),
+                     "alg_bytes_per_launch": (alg / launches) if alg else None,
+                     "achieved_gbs": round(gbs, 2) if gbs else None})
+    rows.sort(key=lambda r: -r["total_ms_per_step"])
+    return rows
+
+
+def cpu_baseline(img, m, depth, budget_s=12.0, max_reps=10):
+    """The C oracle (same algorithm and complexity as cv::watershed + colorByIndexes), serial,
+    on the SAME frame, repeated until ~budget_s of CPU work."""
+    from oracle import ws_oracle
+
+    H, W = m.shape
+    reps, t_tot = 0, 0.0
+    while reps < max_reps and t_tot < budget_s:
+        t0 = time.perf_counter()
+        lab = ws_oracle.watershed(img, m)
+        ws_oracle.colorize(lab, depth, None)
+        t_tot += time.perf_counter() - t0
+        reps += 1
+    return {"value": round(H * W * reps / t_tot / 1e6, 3), "unit": "Mpx/s", "cores": 1, "kind": "port",
+            "sample": "%d full %dx%d frame(s): oracle/ws_oracle.c watershed + colorize, 1 thread, %.1f s"
+                      % (reps, H, W, t_tot)}, lab
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--kind", default="mosaic", choices=["mosaic", "mosaic_noise", "random"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile-pass", action="store_true")
+    args = ap.parse_args(argv)
+
+    rank, world, local = dist_env()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import msegment
+    from msegment import synth
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    barrier = (lambda: dist.barrier()) if world > 1 else (lambda: None)
+    sync = torch.cuda.synchronize
+
+    S = args.size
+    seed = 2 if world == 1 else 100 + rank
+    t0 = time.perf_counter()
+    img, m, depth = synth.frame(args.kind, S, S, seed)
+    log("[rank %d] generated %s %dx%d seed %d in %.1fs" % (rank, args.kind, S, S, seed, time.perf_counter() - t0))
+    t_img = torch.from_numpy(img).to(dev)
+    t_m = torch.from_numpy(m).to(dev)
+    t_lab = torch.empty_like(t_m)
+    t_dst = torch.empty((S, S, 3), dtype=torch.uint8, device=dev)
+    seg = msegment.Segmenter(local)
+
+    def step():
+        seg.watershed_colorize_dev(t_img, t_m, t_lab, depth, None, t_dst)
+
+    for _ in range(args.warmup):
+        step()
+    sync()
+    st = seg.stats()
+    parity = None
+    if rank == 0 and args.kind == "mosaic" and S == 4096 and seed == 2:
+        dg = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))["mosaic_4096x4096_s2"]
+        got = hashlib.sha256(t_lab.cpu().numpy().tobytes()).hexdigest()
+        parity = "bit-exact vs oracle digest" if got == dg["labels_sha256"] else "MISMATCH vs oracle digest"
+        log("[rank 0] parity:", parity)
+
+    dt = timed_steps(step, args.steps, barrier, sync)
+    dt_max = reduce_max(dt, dev)
+    value = world * S * S * args.steps / dt_max / 1e6
+    ms_per_step = 1000.0 * dt_max / args.steps
+    log("[rank %d] %.3f ms/step (max over ranks %.3f)" % (rank, 1000 * dt / args.steps, ms_per_step))
+
+    kern = None
+    if not args.no_profile_pass:
+        seg.set_profiling(True)
+        seg.kernel_profile(reset=True)
+        for _ in range(args.steps):
+            step()
+        sync()
+        prof = seg.kernel_profile(reset=True)
+        seg.set_profiling(False)
+        kern = kernel_roofline(prof, st, S * S, args.steps)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, cpu_lab = cpu_baseline(img, m, depth)
+        if parity is None:
+            parity = "bit-exact vs oracle" if np.array_equal(cpu_lab, t_lab.cpu().numpy()) else "MISMATCH vs oracle"
+
+    if world > 1:
+        barrier()
+    if rank == 0:
+        roof = None
+        if kern:
+            top = kern[0]
+            roof = {"bound": "hbm", "kernel": top["kernel"], "achieved": top["achieved_gbs"],
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(top["achieved_gbs"] / HBM_PEAK_GBS, 5) if top["achieved_gbs"] else None,
+                    "traffic": None,
+                    "alg_bytes_per_launch": top["alg_bytes_per_launch"], "avg_launch_us": top["avg_us"]}
+        e2e_gbs = value * 1e6 * E2E_BYTES_PER_PIXEL / 1e9
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (msegment.synth %s, splitmix64; regenerated on the box)" % args.kind,
+            "config": {"workload": "%s %dx%d seed %s, watershed + colorByIndexes(colored=false), "
+                                   "device-resident (BASELINE config %s)"
+                                   % (args.kind, S, S, "2" if world == 1 else "100+rank", "3" if world == 1 else "5"),
+                       "frames_per_rank_per_step": 1, "parallelism": "replicas%d (no collectives)" % world},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "e2e_hbm": {"achieved": round(e2e_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(e2e_gbs / HBM_PEAK_GBS, 5), "bytes_per_pixel": E2E_BYTES_PER_PIXEL},
+            "flood": {"batches": st["batches"], "pops": st["pops"], "items": st["items"],
+                      "pushes": st["pushes"], "host_syncs": st["host_syncs"]},
+            "kernels": kern,
+            "parity": parity,
+        }
+        print(json.dumps(out), flush=True)
+    seg.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

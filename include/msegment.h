@@ -1,0 +1,127 @@
+/*
+ * msegment.h -- C ABI of libmsegment, the MI355X (gfx950) drop-in for the reference's
+ * watershed hot path.  Plain pointers and sizes only; no exceptions cross this boundary.
+ *
+ * Reference interface each entry point replaces (paths relative to the reference repo):
+ *   PictureService.watershed(Mat src, Mat markers, Integer depth, boolean colored)
+ *       src/main/java/ru/shayhulud/opencvcmsegment/service/PictureService.java:908-911
+ *     = Imgproc.watershed(src, markers)                          PictureService.java:909
+ *       -> static native void watershed_0(long image, long markers)   [ext, OpenCV 3.4.2 Java]
+ *       -> Java_org_opencv_imgproc_Imgproc_watershed_10(JNIEnv*, jclass, jlong, jlong)
+ *       -> cv::watershed(InputArray, InputOutputArray)  modules/imgproc/src/segmentation.cpp
+ *     + colorByIndexes(markers, depth, colored)                   PictureService.java:913-936
+ *       with the palette from generateBGRColor()                  PictureService.java:236-241
+ *     + the callers' cvtColor(dst, COLOR_BGR2GRAY)                PictureService.java:376-379
+ *
+ * Semantics are OpenCV's, bit for bit: markers (int32, rows x cols) are overwritten in place
+ * with the label map (input labels > 0, -1 on watershed lines and on the one-pixel frame, 0 for
+ * interior pixels no seed reaches).  The image is 8-bit 3-channel BGR.
+ *
+ * Return codes: MSG_OK (0) or a negative MSG_E* code; msg_last_error() has the text.
+ * MSG_EINVAL mirrors cv::watershed's CV_Assert (type/size/stride checks); the JNI shim
+ *  turns any nonzero code into a Java exception like CvException.
+ *
+ * Threading: a context is used by one thread at a time; contexts are independent.
+ */
+#ifndef MSEGMENT_H
+#define MSEGMENT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSG_OK        0
+#define MSG_EINVAL   (-1)  /* bad argument: null pointer, negative size, short stride      */
+#define MSG_EHIP     (-2)  /* a HIP runtime call failed                                    */
+#define MSG_ENOMEM   (-3)  /* device allocation failed                                     */
+#define MSG_ETIMEOUT (-4)  /* a bounded in-kernel wait expired (result invalid)            */
+#define MSG_ESTATE   (-5)  /* internal consistency check failed on the device              */
+
+#define MSG_ABI_VERSION 1
+
+typedef struct msg_ctx msg_ctx;
+
+typedef struct msg_stats {
+    int64_t batches;        /* flood generations (bucket batches) in the last watershed call */
+    int64_t pops;           /* pixels popped (labelled or WSHED) in the last call            */
+    int64_t host_syncs;     /* host<->device control round trips in the last call            */
+    int64_t rows, cols;     /* size of the last frame                                        */
+    int64_t items;          /* batch items resolved, committed or not (>= pops)               */
+    int64_t pushes;         /* queue appends after phase 1                                    */
+} msg_stats;
+
+#define MSG_NKERNELS 8
+typedef struct msg_kernel_profile {
+    char    name[32];       /* kernel name, e.g. "k_resolve"                                   */
+    int64_t launches;       /* launches timed since the last reset                              */
+    double  total_ms;       /* sum of HIP-event durations of those launches                     */
+} msg_kernel_profile;
+
+/* One context per thread: owns a HIP stream and the device workspace on `device_ordinal`.
+ * flags: reserved, pass 0.  Replaces: OpenCV.loadLocally()  App.java:15 (library bring-up). */
+int  msg_create(msg_ctx** out, int device_ordinal, unsigned flags);
+void msg_destroy(msg_ctx* ctx);
+const char* msg_last_error(const msg_ctx* ctx);
+int  msg_abi_version(void);
+int  msg_get_stats(const msg_ctx* ctx, msg_stats* out);
+
+/* Per-kernel timing with HIP events recorded on the launch stream around every kernel launch
+ * (measurement aid for bench.py's roofline; off by default).  msg_get_kernel_profile fills up
+ * to max_entries records and returns how many; reset != 0 zeroes the totals. */
+int  msg_set_profiling(msg_ctx* ctx, int enable);
+int  msg_get_kernel_profile(msg_ctx* ctx, msg_kernel_profile* out, int max_entries, int reset);
+
+/* ---- host-buffer entry points (synchronous; strides in BYTES) ---------------------------- */
+
+/* cv::watershed(src, markers) in place.  Replaces Imgproc.watershed  PictureService.java:909. */
+int msg_watershed(msg_ctx* ctx, const uint8_t* bgr, size_t bgr_stride, int32_t* markers,
+                  size_t marker_stride, int rows, int cols);
+
+/* colorByIndexes(labels, depth, colored)  PictureService.java:913-936.
+ * palette_bgr: depth*3 bytes (B,G,R per label 1..depth) = the colored=true palette drawn by
+ * generateBGRColor (PictureService.java:236-241); NULL = colored=false (all white). */
+int msg_colorize(msg_ctx* ctx, const int32_t* labels, size_t label_stride, int rows, int cols,
+                 int depth, const uint8_t* palette_bgr, uint8_t* dst_bgr, size_t dst_stride);
+
+/* PictureService.watershed (PictureService.java:908-911) fused: watershed in place on
+ * `markers`, then colorByIndexes into dst_bgr; if gray != NULL also the callers'
+ * cvtColor(dst, COLOR_BGR2GRAY) (PictureService.java:376-379).  One H2D/D2H per buffer. */
+int msg_watershed_colorize(msg_ctx* ctx, const uint8_t* bgr, size_t bgr_stride,
+                           int32_t* markers, size_t marker_stride, int rows, int cols,
+                           int depth, const uint8_t* palette_bgr, uint8_t* dst_bgr,
+                           size_t dst_stride, uint8_t* gray, size_t gray_stride);
+
+/* Batch of independent frames (BASELINE config 5): frames are processed back to back on this
+ * context's device, no collectives.  Arrays have n entries. */
+int msg_watershed_batch(msg_ctx* ctx, int n, const uint8_t* const* bgr, const size_t* bgr_stride,
+                        int32_t* const* markers, const size_t* marker_stride, const int* rows,
+                        const int* cols);
+
+/* ---- device-resident entry points (dense layouts; pointers are device memory of the
+ * context's device; stream = hipStream_t or NULL for the context's own stream).  They return
+ * when the flood has finished; the colourise kernel may still be in flight on `stream`. ---- */
+
+/* d_markers_in (int32) is read, d_labels (int32) written; they may alias (in place). */
+int msg_watershed_dev(msg_ctx* ctx, const void* d_bgr, const void* d_markers_in, void* d_labels,
+                      int rows, int cols, void* stream);
+
+int msg_colorize_dev(msg_ctx* ctx, const void* d_labels, int rows, int cols, int depth,
+                     const void* d_palette_bgr, void* d_dst_bgr, void* d_gray, void* stream);
+
+int msg_watershed_colorize_dev(msg_ctx* ctx, const void* d_bgr, const void* d_markers_in,
+                               void* d_labels, int rows, int cols, int depth,
+                               const void* d_palette_bgr, void* d_dst_bgr, void* d_gray,
+                               void* stream);
+
+/* Stencil only: L-inf BGR distance to the right and lower neighbour (uint8 each, 0 past the
+ * edge) -- the colour-distance kernel of the flood, exposed for parity tests and the roofline. */
+int msg_edge_weights_dev(msg_ctx* ctx, const void* d_bgr, void* d_wright, void* d_wdown,
+                         int rows, int cols, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MSEGMENT_H */

@@ -1,0 +1,540 @@
+// msegment_capi.hip -- host engine + C ABI of libmsegment (see include/msegment.h).
+//
+// One translation unit with the kernels (no relocatable device code needed).  The flood is
+// driven from the host as a stream of fixed 3-kernel iterations (resolve -> scan -> scatter);
+// every kernel reads the current batch from the device control block, so the host never needs
+// the batch size: it only polls a pinned "done" word once per group of iterations, with one
+// group always queued ahead so the GPU never idles on the poll.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstddef>
+#include <cstring>
+#include <new>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/msegment.h"
+#include "ws_kernels.hip"
+
+using namespace msg;
+
+struct msg_ctx {
+  int dev = 0;
+  hipStream_t own = nullptr;
+  std::string err;
+  Ctl* d_ctl = nullptr;
+  // flood workspace (sized for cap_n pixels)
+  long long cap_n = 0;
+  uint8_t *d_wr = nullptr, *d_wd = nullptr, *d_lv1 = nullptr;
+  int32_t *d_qpos = nullptr, *d_qbuf = nullptr, *d_ilist = nullptr;
+  int32_t *d_cnt = nullptr, *d_coff = nullptr, *d_tot = nullptr, *d_choff = nullptr;
+  unsigned long long *d_tl = nullptr, *d_desc = nullptr;
+  long long qcap = 0;
+  // staging for the host-buffer entry points
+  long long stage_n = 0;
+  uint8_t* d_img = nullptr;
+  int32_t* d_mk = nullptr;
+  uint8_t* d_dst = nullptr;
+  uint8_t* d_gray = nullptr;
+  uint8_t* d_pal = nullptr;
+  size_t pal_cap = 0;
+  // pinned control mirror + events
+  int* h_flags = nullptr;  // [2 slots][4]
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  unsigned epoch = 1;
+  int group = 8;
+  msg_stats stats{};
+  // optional per-kernel HIP-event profiling (msg_set_profiling)
+  bool prof = false;
+  std::vector<hipEvent_t> evpool;
+  size_t evused = 0;
+  std::vector<std::pair<int, size_t>> recs;  // (kernel id, index of the start event)
+  double prof_ms[MSG_NKERNELS] = {};
+  long long prof_n[MSG_NKERNELS] = {};
+};
+
+namespace {
+
+enum KernelId { KID_PREP, KID_INIT_SCAN, KID_COMPACT, KID_RESOLVE, KID_SCAN, KID_SCATTER,
+                KID_COLORIZE, KID_EDGE };
+const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_compact", "k_resolve",
+                                                "k_scan", "k_scatter", "k_colorize",
+                                                "k_edge_weights"};
+
+hipEvent_t pool_event(msg_ctx* c) {
+  if (c->evused == c->evpool.size()) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    c->evpool.push_back(e);
+  }
+  return c->evpool[c->evused++];
+}
+
+// Launch with optional start/stop events on the launch stream.
+#define LAUNCH(c, kid, st, kern, grid, block, shm, ...)                                     \
+  do {                                                                                   \
+    size_t i0_ = 0;                                                                      \
+    if ((c)->prof) {                                                                     \
+      i0_ = (c)->evused;                                                                 \
+      hipEvent_t a_ = pool_event(c), b_ = pool_event(c);                                 \
+      if (a_ && b_) (void)hipEventRecord(a_, st);                                        \
+      else (c)->prof = false;                                                            \
+    }                                                                                    \
+    hipLaunchKernelGGL(kern, grid, block, shm, st, __VA_ARGS__);                         \
+    if ((c)->prof) {                                                                     \
+      (void)hipEventRecord((c)->evpool[i0_ + 1], st);                                    \
+      (c)->recs.emplace_back((int)(kid), i0_);                                           \
+    }                                                                                    \
+  } while (0)
+
+// Fold recorded event pairs into the per-kernel totals (stream must be synchronised).
+void collect_profile(msg_ctx* c) {
+  for (auto& r : c->recs) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, c->evpool[r.second], c->evpool[r.second + 1]) == hipSuccess) {
+      c->prof_ms[r.first] += ms;
+      c->prof_n[r.first] += 1;
+    }
+  }
+  c->recs.clear();
+  c->evused = 0;
+}
+
+int fail(msg_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(c, call)                                                                      \
+  do {                                                                                       \
+    hipError_t e_ = (call);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      return fail((c), e_ == hipErrorOutOfMemory ? MSG_ENOMEM : MSG_EHIP, "%s: %s (%s:%d)", \
+                  #call, hipGetErrorString(e_), __FILE__, __LINE__);                         \
+  } while (0)
+
+template <class T>
+void dfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+void free_flood(msg_ctx* c) {
+  dfree(c->d_wr); dfree(c->d_wd); dfree(c->d_lv1);
+  dfree(c->d_qpos); dfree(c->d_qbuf); dfree(c->d_ilist);
+  dfree(c->d_cnt); dfree(c->d_coff); dfree(c->d_tot); dfree(c->d_choff);
+  dfree(c->d_tl); dfree(c->d_desc);
+  c->cap_n = 0;
+  c->qcap = 0;
+}
+
+void free_stage(msg_ctx* c) {
+  dfree(c->d_img); dfree(c->d_mk); dfree(c->d_dst); dfree(c->d_gray);
+  c->stage_n = 0;
+}
+
+int ensure_flood(msg_ctx* c, long long N) {
+  if (N <= c->cap_n) return MSG_OK;
+  free_flood(c);
+  const long long nch = (N + CH - 1) / CH;
+  const long long qcap = 4 * N + 16;
+  HIPCHK(c, hipMalloc((void**)&c->d_wr, N));
+  HIPCHK(c, hipMalloc((void**)&c->d_wd, N));
+  HIPCHK(c, hipMalloc((void**)&c->d_lv1, N));
+  HIPCHK(c, hipMalloc((void**)&c->d_qpos, N * 4));
+  HIPCHK(c, hipMalloc((void**)&c->d_ilist, N * 4));
+  HIPCHK(c, hipMalloc((void**)&c->d_qbuf, qcap * 4));
+  HIPCHK(c, hipMalloc((void**)&c->d_tl, N * 8));
+  HIPCHK(c, hipMalloc((void**)&c->d_desc, N * 8));
+  HIPCHK(c, hipMalloc((void**)&c->d_cnt, nch * NQ * 4));
+  HIPCHK(c, hipMalloc((void**)&c->d_coff, nch * NQ * 4));
+  HIPCHK(c, hipMalloc((void**)&c->d_tot, nch * 4));
+  HIPCHK(c, hipMalloc((void**)&c->d_choff, nch * 4));
+  HIPCHK(c, hipMemset(c->d_tl, 0, N * 8));
+  c->epoch = 1;
+  c->cap_n = N;
+  c->qcap = qcap;
+  return MSG_OK;
+}
+
+int ensure_stage(msg_ctx* c, long long N) {
+  if (N <= c->stage_n) return MSG_OK;
+  free_stage(c);
+  HIPCHK(c, hipMalloc((void**)&c->d_img, N * 3 + 16));
+  HIPCHK(c, hipMalloc((void**)&c->d_mk, N * 4 + 16));
+  HIPCHK(c, hipMalloc((void**)&c->d_dst, N * 3 + 16));
+  HIPCHK(c, hipMalloc((void**)&c->d_gray, N + 16));
+  c->stage_n = N;
+  return MSG_OK;
+}
+
+int check_size(msg_ctx* c, int rows, int cols) {
+  if (rows < 0 || cols < 0) return fail(c, MSG_EINVAL, "negative size %d x %d", rows, cols);
+  if ((long long)rows * cols >= 0x7fffffffll / 4)
+    return fail(c, MSG_EINVAL, "frame too large for one context: %d x %d", rows, cols);
+  return MSG_OK;
+}
+
+// The exact flood on device buffers.  d_mk_in may alias d_mk.
+int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t* d_mk, int H,
+              int W, hipStream_t st) {
+  const long long N = (long long)H * W;
+  c->stats = msg_stats{};
+  c->stats.rows = H;
+  c->stats.cols = W;
+  if (N == 0) return MSG_OK;
+  int rc = ensure_flood(c, N);
+  if (rc) return rc;
+  if (c->epoch > 0xF0000000u) {
+    HIPCHK(c, hipMemsetAsync(c->d_tl, 0, c->cap_n * 8, st));
+    c->epoch = 1;
+  }
+  Ws ws;
+  ws.img = d_img;
+  ws.mk = d_mk;
+  ws.wr = c->d_wr;
+  ws.wd = c->d_wd;
+  ws.lv1 = c->d_lv1;
+  ws.qpos = c->d_qpos;
+  ws.qbuf = c->d_qbuf;
+  ws.ilist = c->d_ilist;
+  ws.tl = c->d_tl;
+  ws.desc = c->d_desc;
+  ws.cnt = c->d_cnt;
+  ws.coff = c->d_coff;
+  ws.tot = c->d_tot;
+  ws.choff = c->d_choff;
+  ws.ctl = c->d_ctl;
+  ws.H = H;
+  ws.W = W;
+  ws.N = N;
+  ws.qcap = c->qcap;
+
+  const int npx = (int)((N + CH - 1) / CH);
+  const int gres = std::min(npx, RES_GRID_MAX);
+  const int gsc = std::min(npx, 1024);
+  HIPCHK(c, hipMemsetAsync(c->d_ctl, 0, sizeof(Ctl), st));
+  LAUNCH(c, KID_PREP, st, k_prep, dim3(npx), dim3(BS), 0, ws, d_mk_in);
+  LAUNCH(c, KID_INIT_SCAN, st, k_init_scan, dim3(1), dim3(1024), 0, ws, npx, c->epoch);
+  LAUNCH(c, KID_COMPACT, st, k_compact, dim3(npx), dim3(BS), 0, ws);
+  LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws, 1);
+  LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(BS), 0, ws, 1);
+  HIPCHK(c, hipGetLastError());
+
+  int it = 0, slot = 0, prev = -1;
+  long long syncs = 0;
+  for (;;) {
+    for (int g = 0; g < c->group; ++g, ++it) {
+      const int par = it & 1;
+      LAUNCH(c, KID_RESOLVE, st, k_resolve, dim3(gres), dim3(BS), 0, ws, par);
+      LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws, par);
+      LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(BS), 0, ws, par);
+    }
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(c->h_flags + 4 * slot, &c->d_ctl->done, 2 * sizeof(int),
+                             hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipEventRecord(c->ev[slot], st));
+    if (prev >= 0) {
+      HIPCHK(c, hipEventSynchronize(c->ev[prev]));
+      ++syncs;
+      if (c->h_flags[4 * prev] || c->h_flags[4 * prev + 1]) break;
+    }
+    prev = slot;
+    slot ^= 1;
+  }
+  Ctl tail;
+  HIPCHK(c, hipMemcpyAsync(&tail, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  ++syncs;
+  if (c->prof) collect_profile(c);
+  c->stats.batches = tail.batches;
+  c->stats.pops = tail.pops;
+  c->stats.items = tail.items;
+  c->stats.pushes = tail.pushes;
+  c->stats.host_syncs = syncs;
+  c->epoch += (unsigned)std::min<long long>(tail.batches + 4, 0x7fffffff);
+  if (tail.error & ERR_TIMEOUT)
+    return fail(c, MSG_ETIMEOUT, "in-kernel wait timed out (grid not co-resident?)");
+  if (tail.error & ERR_CAPACITY) return fail(c, MSG_ESTATE, "bucket capacity exceeded");
+  if (tail.error) return fail(c, MSG_ESTATE, "device consistency check failed (%d)", tail.error);
+  if (!tail.done) return fail(c, MSG_ESTATE, "flood did not finish");
+  return MSG_OK;
+}
+
+int launch_colorize(msg_ctx* c, const int32_t* d_lab, long long N, int depth, const uint8_t* d_pal,
+                    uint8_t* d_dst, uint8_t* d_gray, hipStream_t st) {
+  if (N == 0) return MSG_OK;
+  const long long th = (N + 3) / 4;
+  const int grid = (int)std::min<long long>((th + 255) / 256, 2048);
+  const size_t shm = (d_pal && depth <= PAL_LDS_MAX) ? (size_t)std::max(depth, 1) * 4 : 0;
+  LAUNCH(c, KID_COLORIZE, st, k_colorize, dim3(grid), dim3(256), shm, d_lab, N, depth, d_pal, d_dst,
+         d_gray);
+  HIPCHK(c, hipGetLastError());
+  return MSG_OK;
+}
+
+int upload_palette(msg_ctx* c, const uint8_t* pal, int depth, hipStream_t st) {
+  const size_t need = (size_t)std::max(depth, 1) * 3;
+  if (need > c->pal_cap) {
+    dfree(c->d_pal);
+    HIPCHK(c, hipMalloc((void**)&c->d_pal, need));
+    c->pal_cap = need;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_pal, pal, (size_t)depth * 3, hipMemcpyHostToDevice, st));
+  return MSG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int msg_abi_version(void) { return MSG_ABI_VERSION; }
+
+int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
+  (void)flags;
+  if (!out) return MSG_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MSG_EHIP;
+  if (device_ordinal < 0 || device_ordinal >= ndev) return MSG_EINVAL;
+  msg_ctx* c = new (std::nothrow) msg_ctx();
+  if (!c) return MSG_ENOMEM;
+  c->dev = device_ordinal;
+  if (hipSetDevice(c->dev) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void**)&c->d_ctl, sizeof(Ctl)) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_flags, 8 * sizeof(int), hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev[1], hipEventDisableTiming) != hipSuccess) {
+    msg_destroy(c);
+    return MSG_EHIP;
+  }
+  *out = c;
+  return MSG_OK;
+}
+
+void msg_destroy(msg_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->dev);
+  if (c->own) (void)hipStreamSynchronize(c->own);
+  free_flood(c);
+  free_stage(c);
+  dfree(c->d_pal);
+  dfree(c->d_ctl);
+  if (c->h_flags) (void)hipHostFree(c->h_flags);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->evpool) (void)hipEventDestroy(e);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+}
+
+const char* msg_last_error(const msg_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int msg_get_stats(const msg_ctx* c, msg_stats* out) {
+  if (!c || !out) return MSG_EINVAL;
+  *out = c->stats;
+  return MSG_OK;
+}
+
+int msg_set_profiling(msg_ctx* c, int enable) {
+  if (!c) return MSG_EINVAL;
+  c->prof = enable != 0;
+  return MSG_OK;
+}
+
+int msg_get_kernel_profile(msg_ctx* c, msg_kernel_profile* out, int max_entries, int reset) {
+  if (!c || (max_entries > 0 && !out)) return MSG_EINVAL;
+  if (!c->recs.empty()) {
+    (void)hipSetDevice(c->dev);
+    (void)hipDeviceSynchronize();
+    collect_profile(c);
+  }
+  int n = 0;
+  for (int k = 0; k < MSG_NKERNELS && n < max_entries; ++k) {
+    std::snprintf(out[n].name, sizeof(out[n].name), "%s", kKernelNames[k]);
+    out[n].launches = c->prof_n[k];
+    out[n].total_ms = c->prof_ms[k];
+    ++n;
+  }
+  if (reset) {
+    for (int k = 0; k < MSG_NKERNELS; ++k) {
+      c->prof_ms[k] = 0;
+      c->prof_n[k] = 0;
+    }
+  }
+  return n;
+}
+
+int msg_watershed_dev(msg_ctx* c, const void* d_bgr, const void* d_markers_in, void* d_labels,
+                      int rows, int cols, void* stream) {
+  if (!c) return MSG_EINVAL;
+  int rc = check_size(c, rows, cols);
+  if (rc) return rc;
+  if ((long long)rows * cols > 0 && (!d_bgr || !d_markers_in || !d_labels))
+    return fail(c, MSG_EINVAL, "null device pointer");
+  HIPCHK(c, hipSetDevice(c->dev));
+  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  return run_flood(c, (const uint8_t*)d_bgr, (const int32_t*)d_markers_in, (int32_t*)d_labels,
+                   rows, cols, st);
+}
+
+int msg_colorize_dev(msg_ctx* c, const void* d_labels, int rows, int cols, int depth,
+                     const void* d_palette_bgr, void* d_dst_bgr, void* d_gray, void* stream) {
+  if (!c) return MSG_EINVAL;
+  int rc = check_size(c, rows, cols);
+  if (rc) return rc;
+  if (depth < 0) return fail(c, MSG_EINVAL, "negative depth");
+  if ((long long)rows * cols > 0 && (!d_labels || !d_dst_bgr))
+    return fail(c, MSG_EINVAL, "null device pointer");
+  HIPCHK(c, hipSetDevice(c->dev));
+  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  return launch_colorize(c, (const int32_t*)d_labels, (long long)rows * cols, depth,
+                         (const uint8_t*)d_palette_bgr, (uint8_t*)d_dst_bgr, (uint8_t*)d_gray, st);
+}
+
+int msg_watershed_colorize_dev(msg_ctx* c, const void* d_bgr, const void* d_markers_in,
+                               void* d_labels, int rows, int cols, int depth,
+                               const void* d_palette_bgr, void* d_dst_bgr, void* d_gray,
+                               void* stream) {
+  int rc = msg_watershed_dev(c, d_bgr, d_markers_in, d_labels, rows, cols, stream);
+  if (rc) return rc;
+  return msg_colorize_dev(c, d_labels, rows, cols, depth, d_palette_bgr, d_dst_bgr, d_gray, stream);
+}
+
+int msg_edge_weights_dev(msg_ctx* c, const void* d_bgr, void* d_wright, void* d_wdown, int rows,
+                         int cols, void* stream) {
+  if (!c) return MSG_EINVAL;
+  int rc = check_size(c, rows, cols);
+  if (rc) return rc;
+  const long long N = (long long)rows * cols;
+  if (N == 0) return MSG_OK;
+  if (!d_bgr || !d_wright || !d_wdown) return fail(c, MSG_EINVAL, "null device pointer");
+  HIPCHK(c, hipSetDevice(c->dev));
+  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  const long long th = (N + 3) / 4;
+  LAUNCH(c, KID_EDGE, st, k_edge_weights, dim3((unsigned)((th + 255) / 256)), dim3(256), 0,
+         (const uint8_t*)d_bgr, (uint8_t*)d_wright, (uint8_t*)d_wdown, rows, cols);
+  HIPCHK(c, hipGetLastError());
+  return MSG_OK;
+}
+
+static int host_args(msg_ctx* c, const void* bgr, size_t bgr_stride, const void* markers,
+                     size_t marker_stride, int rows, int cols) {
+  if (!c) return MSG_EINVAL;
+  int rc = check_size(c, rows, cols);
+  if (rc) return rc;
+  if ((long long)rows * cols == 0) return MSG_OK;
+  if (!bgr || !markers) return fail(c, MSG_EINVAL, "null host pointer");
+  if (bgr_stride < (size_t)cols * 3) return fail(c, MSG_EINVAL, "bgr stride too small");
+  if (marker_stride < (size_t)cols * 4 || (marker_stride & 3))
+    return fail(c, MSG_EINVAL, "marker stride invalid");
+  return MSG_OK;
+}
+
+int msg_watershed_colorize(msg_ctx* c, const uint8_t* bgr, size_t bgr_stride, int32_t* markers,
+                           size_t marker_stride, int rows, int cols, int depth,
+                           const uint8_t* palette_bgr, uint8_t* dst_bgr, size_t dst_stride,
+                           uint8_t* gray, size_t gray_stride) {
+  int rc = host_args(c, bgr, bgr_stride, markers, marker_stride, rows, cols);
+  if (rc) return rc;
+  const long long N = (long long)rows * cols;
+  if (N == 0) return MSG_OK;
+  const bool want_color = dst_bgr != nullptr;
+  if (want_color) {
+    if (depth < 0) return fail(c, MSG_EINVAL, "negative depth");
+    if (dst_stride < (size_t)cols * 3) return fail(c, MSG_EINVAL, "dst stride too small");
+    if (gray && gray_stride < (size_t)cols) return fail(c, MSG_EINVAL, "gray stride too small");
+  }
+  HIPCHK(c, hipSetDevice(c->dev));
+  rc = ensure_stage(c, N);
+  if (rc) return rc;
+  hipStream_t st = c->own;
+  HIPCHK(c, hipMemcpy2DAsync(c->d_img, (size_t)cols * 3, bgr, bgr_stride, (size_t)cols * 3, rows,
+                             hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpy2DAsync(c->d_mk, (size_t)cols * 4, markers, marker_stride, (size_t)cols * 4,
+                             rows, hipMemcpyHostToDevice, st));
+  rc = run_flood(c, c->d_img, c->d_mk, c->d_mk, rows, cols, st);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpy2DAsync(markers, marker_stride, c->d_mk, (size_t)cols * 4, (size_t)cols * 4,
+                             rows, hipMemcpyDeviceToHost, st));
+  if (want_color) {
+    const uint8_t* dp = nullptr;
+    if (palette_bgr && depth > 0) {
+      rc = upload_palette(c, palette_bgr, depth, st);
+      if (rc) return rc;
+      dp = c->d_pal;
+    } else if (palette_bgr) {
+      dp = nullptr;  // depth 0: every pixel is background either way
+    }
+    rc = launch_colorize(c, c->d_mk, N, depth, dp, c->d_dst, gray ? c->d_gray : nullptr, st);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpy2DAsync(dst_bgr, dst_stride, c->d_dst, (size_t)cols * 3, (size_t)cols * 3,
+                               rows, hipMemcpyDeviceToHost, st));
+    if (gray)
+      HIPCHK(c, hipMemcpy2DAsync(gray, gray_stride, c->d_gray, (size_t)cols, (size_t)cols, rows,
+                                 hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(c, hipStreamSynchronize(st));
+  return MSG_OK;
+}
+
+int msg_watershed(msg_ctx* c, const uint8_t* bgr, size_t bgr_stride, int32_t* markers,
+                  size_t marker_stride, int rows, int cols) {
+  return msg_watershed_colorize(c, bgr, bgr_stride, markers, marker_stride, rows, cols, 0, nullptr,
+                                nullptr, 0, nullptr, 0);
+}
+
+int msg_colorize(msg_ctx* c, const int32_t* labels, size_t label_stride, int rows, int cols,
+                 int depth, const uint8_t* palette_bgr, uint8_t* dst_bgr, size_t dst_stride) {
+  if (!c) return MSG_EINVAL;
+  int rc = check_size(c, rows, cols);
+  if (rc) return rc;
+  const long long N = (long long)rows * cols;
+  if (N == 0) return MSG_OK;
+  if (depth < 0) return fail(c, MSG_EINVAL, "negative depth");
+  if (!labels || !dst_bgr) return fail(c, MSG_EINVAL, "null host pointer");
+  if (label_stride < (size_t)cols * 4 || (label_stride & 3) || dst_stride < (size_t)cols * 3)
+    return fail(c, MSG_EINVAL, "stride invalid");
+  HIPCHK(c, hipSetDevice(c->dev));
+  rc = ensure_stage(c, N);
+  if (rc) return rc;
+  hipStream_t st = c->own;
+  HIPCHK(c, hipMemcpy2DAsync(c->d_mk, (size_t)cols * 4, labels, label_stride, (size_t)cols * 4,
+                             rows, hipMemcpyHostToDevice, st));
+  const uint8_t* dp = nullptr;
+  if (palette_bgr && depth > 0) {
+    rc = upload_palette(c, palette_bgr, depth, st);
+    if (rc) return rc;
+    dp = c->d_pal;
+  }
+  rc = launch_colorize(c, c->d_mk, N, depth, dp, c->d_dst, nullptr, st);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpy2DAsync(dst_bgr, dst_stride, c->d_dst, (size_t)cols * 3, (size_t)cols * 3,
+                             rows, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  return MSG_OK;
+}
+
+int msg_watershed_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size_t* bgr_stride,
+                        int32_t* const* markers, const size_t* marker_stride, const int* rows,
+                        const int* cols) {
+  if (!c || n < 0) return MSG_EINVAL;
+  if (n > 0 && (!bgr || !bgr_stride || !markers || !marker_stride || !rows || !cols))
+    return fail(c, MSG_EINVAL, "null batch array");
+  for (int k = 0; k < n; ++k) {
+    int rc = msg_watershed(c, bgr[k], bgr_stride[k], markers[k], marker_stride[k], rows[k], cols[k]);
+    if (rc) return rc;
+  }
+  return MSG_OK;
+}
+
+}  // extern "C"

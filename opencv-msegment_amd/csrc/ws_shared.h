@@ -1,0 +1,70 @@
+// ws_shared.h -- types shared by the gfx950 kernels (ws_kernels.hip) and the host engine
+// (msegment_capi.hip).  See ws_kernels.hip for the algorithm and the HBM layout.
+#pragma once
+#include <stdint.h>
+
+namespace msg {
+
+constexpr int NQ = 256;          // bucket levels = L-inf BGR distances 0..255 (cv::watershed NQ)
+constexpr int BS = 256;          // threads per block of the chunk kernels
+constexpr int CH = 4096;         // items per chunk of the ordered multi-bucket append
+constexpr int SUB = CH / BS;     // sub-rounds per chunk
+constexpr int WSHED = -1;        // cv::watershed WSHED
+constexpr int INQ = -2;          // cv::watershed IN_QUEUE
+constexpr int NONE = 0x7fffffff;
+constexpr int RES_GRID_MAX = 512;  // <= 2 blocks of 256 threads per CU: all co-resident
+constexpr int PAL_LDS_MAX = 16384; // palettes up to this many labels are staged in LDS
+constexpr long long SPIN_LIMIT_TICKS = 200000000ll;  // 2 s of s_memrealtime (100 MHz)
+
+constexpr int ERR_TIMEOUT = 1;
+constexpr int ERR_STATE = 2;
+constexpr int ERR_CAPACITY = 4;
+
+struct Batch {
+  int L;           // bucket level (-1 for the phase-1 pseudo-batch)
+  int bstart;      // absolute qbuf slot of rank 0
+  int n;           // items in the batch (0 = nothing to do / finished)
+  unsigned epoch;  // tag of this batch's tl granules
+  int ncommit;     // committed prefix (set by k_scan)
+  int nchunk;      // chunks of the committed prefix (set by k_scan)
+  int mode;        // 0 = flood batch, 1 = phase-1 pseudo-batch (items = ilist)
+  int pad;
+};
+
+struct Ctl {
+  int qbase[NQ + 1];
+  int qhead[NQ];
+  int qtail[NQ];
+  unsigned cap[NQ];
+  Batch bat[2];
+  int cut[2];
+  int done;
+  int error;
+  long long batches;
+  long long pops;
+  long long items;   // sum of batch sizes resolved (committed or not)
+  long long pushes;  // committed pushes appended to buckets
+};
+
+struct Ws {
+  const uint8_t* img;
+  int32_t* mk;
+  uint8_t* wr;
+  uint8_t* wd;
+  uint8_t* lv1;
+  int32_t* qpos;
+  int32_t* qbuf;
+  int32_t* ilist;
+  unsigned long long* tl;
+  unsigned long long* desc;
+  int32_t* cnt;
+  int32_t* coff;
+  int32_t* tot;
+  int32_t* choff;
+  Ctl* ctl;
+  int H, W;
+  long long N;
+  long long qcap;
+};
+
+}  // namespace msg

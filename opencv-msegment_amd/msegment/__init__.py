@@ -1,0 +1,214 @@
+"""msegment -- MI355X-native drop-in for the reference's watershed hot path.
+
+Host-side mirror of the reference interface over libmsegment.so (include/msegment.h):
+
+* :class:`Segmenter` -- one libmsegment context (one HIP stream + device workspace).
+  ``watershed`` is ``Imgproc.watershed(src, markers)`` (PictureService.java:909): markers are
+  rewritten IN PLACE with OpenCV's exact label map; ``colorize`` is ``colorByIndexes``
+  (PictureService.java:913-936).
+* :class:`PictureService` (picture_service.py) -- ``watershed(src, markers, depth, colored)``
+  exactly as ``PictureService.watershed`` (PictureService.java:908-911).
+
+Errors raise :class:`MsegError` (the ``CvException`` analogue); a missing HIP library raises
+ImportError -- there is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import MsegError, Stats
+
+__all__ = ["Segmenter", "MsegError", "Stats", "PictureService"]
+
+
+def _vp(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def _img_view(bgr):
+    bgr = np.asarray(bgr)
+    if bgr.dtype != np.uint8 or bgr.ndim != 3 or bgr.shape[2] != 3:
+        raise MsegError(_lib.MSG_EINVAL, "src must be uint8 (H, W, 3) BGR (CV_8UC3)")
+    if bgr.strides[2] != 1 or bgr.strides[1] != 3 or bgr.strides[0] < 0:
+        bgr = np.ascontiguousarray(bgr)
+    return bgr, bgr.strides[0] if bgr.shape[0] > 0 else bgr.shape[1] * 3
+
+
+class Segmenter:
+    """One libmsegment context on HIP device ``device``."""
+
+    def __init__(self, device=0):
+        self._L = _lib.load()
+        h = ctypes.c_void_p()
+        rc = self._L.msg_create(ctypes.byref(h), int(device), 0)
+        if rc != 0:
+            raise MsegError(rc, "msg_create(device=%d) failed" % device)
+        self._h = h
+        self.device = device
+
+    # -- plumbing -------------------------------------------------------------------------
+    def _check(self, rc):
+        if rc != 0:
+            raise MsegError(rc, self._L.msg_last_error(self._h).decode(errors="replace"))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.msg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_profiling(self, on=True):
+        self._check(self._L.msg_set_profiling(self._h, 1 if on else 0))
+
+    def kernel_profile(self, reset=True):
+        """{kernel: (launches, total_ms)} from HIP events on the launch stream."""
+        arr = (_lib.KernelProfile * _lib.NKERNELS)()
+        n = self._L.msg_get_kernel_profile(self._h, arr, _lib.NKERNELS, 1 if reset else 0)
+        if n < 0:
+            self._check(n)
+        return {arr[k].name.decode(): (arr[k].launches, arr[k].total_ms) for k in range(n)}
+
+    def stats(self):
+        s = Stats()
+        self._check(self._L.msg_get_stats(self._h, ctypes.byref(s)))
+        return {k: getattr(s, k) for k, _ in Stats._fields_}
+
+    # -- host buffers (numpy) -------------------------------------------------------------
+    def watershed(self, bgr, markers):
+        """cv::watershed(bgr, markers): ``markers`` (int32 (H, W) ndarray) is rewritten in place."""
+        self.watershed_colorize(bgr, markers, None)
+        return markers
+
+    def watershed_colorize(self, bgr, markers, depth, palette=None, gray=False):
+        """Fused PictureService.watershed: labels in place, then colorByIndexes (+ BGR2GRAY).
+
+        ``depth=None`` skips the colourise step.  ``palette`` = (depth, 3) uint8 BGR or None
+        (colored=false: white).  Returns dst or (dst, gray)."""
+        bgr, bstride = _img_view(bgr)
+        if not isinstance(markers, np.ndarray) or markers.dtype != np.int32 or markers.ndim != 2:
+            raise MsegError(_lib.MSG_EINVAL, "markers must be an int32 (H, W) ndarray (CV_32SC1)")
+        H, W = markers.shape
+        if bgr.shape[:2] != (H, W):
+            raise MsegError(_lib.MSG_EINVAL, "src and markers sizes differ")
+        work = markers
+        if markers.strides[1] != 4 or markers.strides[0] < W * 4 or not markers.flags.writeable:
+            work = np.ascontiguousarray(markers)
+        mstride = work.strides[0] if H > 0 else W * 4
+        dst = gr = pal = None
+        if depth is not None:
+            depth = int(depth)
+            dst = np.empty((H, W, 3), dtype=np.uint8)
+            if gray:
+                gr = np.empty((H, W), dtype=np.uint8)
+            if palette is not None:
+                pal = np.ascontiguousarray(palette, dtype=np.uint8).reshape(-1, 3)
+                if pal.shape[0] < depth:
+                    raise MsegError(_lib.MSG_EINVAL, "palette has fewer than depth colours")
+        rc = self._L.msg_watershed_colorize(
+            self._h, _vp(bgr), bstride, _vp(work), mstride, H, W,
+            depth if depth is not None else 0, _vp(pal), _vp(dst), W * 3, _vp(gr), W)
+        self._check(rc)
+        if work is not markers:
+            markers[...] = work
+        if depth is None:
+            return markers
+        return (dst, gr) if gray else dst
+
+    def colorize(self, labels, depth, palette=None):
+        """colorByIndexes(labels, depth, colored) -> (H, W, 3) uint8."""
+        labels = np.ascontiguousarray(labels, dtype=np.int32)
+        H, W = labels.shape
+        dst = np.empty((H, W, 3), dtype=np.uint8)
+        pal = None
+        if palette is not None:
+            pal = np.ascontiguousarray(palette, dtype=np.uint8).reshape(-1, 3)
+        self._check(self._L.msg_colorize(self._h, _vp(labels), W * 4, H, W, int(depth), _vp(pal),
+                                         _vp(dst), W * 3))
+        return dst
+
+    def watershed_batch(self, frames):
+        """frames: list of (bgr, markers); every markers array is rewritten in place."""
+        n = len(frames)
+        keep = []
+        bp = (ctypes.c_void_p * n)()
+        bs = (ctypes.c_size_t * n)()
+        mp = (ctypes.c_void_p * n)()
+        ms = (ctypes.c_size_t * n)()
+        rows = (ctypes.c_int * n)()
+        cols = (ctypes.c_int * n)()
+        for k, (bgr, m) in enumerate(frames):
+            bgr, st = _img_view(bgr)
+            if m.dtype != np.int32 or not m.flags.c_contiguous:
+                raise MsegError(_lib.MSG_EINVAL, "batch markers must be C-contiguous int32")
+            keep.append(bgr)
+            bp[k] = bgr.ctypes.data
+            bs[k] = st
+            mp[k] = m.ctypes.data
+            ms[k] = m.shape[1] * 4
+            rows[k], cols[k] = m.shape
+        self._check(self._L.msg_watershed_batch(self._h, n, bp, bs, mp, ms, rows, cols))
+
+    # -- device-resident buffers (torch tensors on this device) ---------------------------
+    @staticmethod
+    def _stream(stream):
+        if stream is None:
+            import torch
+            return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        return ctypes.c_void_p(int(stream))
+
+    def watershed_dev(self, bgr, markers_in, labels=None, stream=None):
+        """Device-resident flood: uint8 (H, W, 3) + int32 (H, W) -> int32 labels (may alias)."""
+        H, W = markers_in.shape
+        if labels is None:
+            labels = markers_in
+        for t in (bgr, markers_in, labels):
+            if not t.is_contiguous():
+                raise MsegError(_lib.MSG_EINVAL, "device tensors must be contiguous")
+        self._check(self._L.msg_watershed_dev(self._h, ctypes.c_void_p(bgr.data_ptr()),
+                                              ctypes.c_void_p(markers_in.data_ptr()),
+                                              ctypes.c_void_p(labels.data_ptr()), H, W,
+                                              self._stream(stream)))
+        return labels
+
+    def colorize_dev(self, labels, depth, palette=None, dst=None, gray=None, stream=None):
+        H, W = labels.shape
+        self._check(self._L.msg_colorize_dev(
+            self._h, ctypes.c_void_p(labels.data_ptr()), H, W, int(depth),
+            ctypes.c_void_p(palette.data_ptr()) if palette is not None else None,
+            ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(gray.data_ptr()) if gray is not None else None,
+            self._stream(stream)))
+        return dst
+
+    def watershed_colorize_dev(self, bgr, markers_in, labels, depth, palette, dst, gray=None,
+                               stream=None):
+        H, W = markers_in.shape
+        self._check(self._L.msg_watershed_colorize_dev(
+            self._h, ctypes.c_void_p(bgr.data_ptr()), ctypes.c_void_p(markers_in.data_ptr()),
+            ctypes.c_void_p(labels.data_ptr()), H, W, int(depth),
+            ctypes.c_void_p(palette.data_ptr()) if palette is not None else None,
+            ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(gray.data_ptr()) if gray is not None else None,
+            self._stream(stream)))
+        return dst
+
+    def edge_weights_dev(self, bgr, wright, wdown, stream=None):
+        H, W = bgr.shape[:2]
+        self._check(self._L.msg_edge_weights_dev(self._h, ctypes.c_void_p(bgr.data_ptr()),
+                                                 ctypes.c_void_p(wright.data_ptr()),
+                                                 ctypes.c_void_p(wdown.data_ptr()), H, W,
+                                                 self._stream(stream)))
+        return wright, wdown
+
+
+from .picture_service import PictureService  # noqa: E402

@@ -1,0 +1,101 @@
+"""ctypes binding of libmsegment.so (the C ABI declared in include/msegment.h).
+
+There is deliberately NO fallback: if the HIP library is missing or fails to load, every entry
+point raises.  The CPU restatement under oracle/ is test infrastructure and is never imported
+here.
+"""
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmsegment.so")
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+
+MSG_OK = 0
+MSG_EINVAL = -1
+MSG_EHIP = -2
+MSG_ENOMEM = -3
+MSG_ETIMEOUT = -4
+MSG_ESTATE = -5
+
+# every symbol include/msegment.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "msg_create", "msg_destroy", "msg_last_error", "msg_abi_version", "msg_get_stats",
+    "msg_watershed", "msg_colorize", "msg_watershed_colorize", "msg_watershed_batch",
+    "msg_watershed_dev", "msg_colorize_dev", "msg_watershed_colorize_dev", "msg_edge_weights_dev",
+    "msg_set_profiling", "msg_get_kernel_profile",
+)
+
+
+class MsegError(RuntimeError):
+    """Raised for a nonzero libmsegment return code (the CvException analogue)."""
+
+    def __init__(self, code, msg):
+        super().__init__("libmsegment error %d: %s" % (code, msg))
+        self.code = code
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_int64), ("pops", ctypes.c_int64),
+                ("host_syncs", ctypes.c_int64), ("rows", ctypes.c_int64), ("cols", ctypes.c_int64),
+                ("items", ctypes.c_int64), ("pushes", ctypes.c_int64)]
+
+
+class KernelProfile(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int64), ("total_ms", ctypes.c_double)]
+
+
+NKERNELS = 8
+
+
+def build(arch="gfx950"):
+    """Compile libmsegment.so in-tree with hipcc (no GPU needed)."""
+    subprocess.check_call(["make", "-s", "-C", CSRC, "ARCH=%s" % arch])
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libmsegment.so not built at %s (run __graft_entry__.build())" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    sz = ctypes.c_size_t
+    i = ctypes.c_int
+    L.msg_create.argtypes = [ctypes.POINTER(vp), i, ctypes.c_uint]
+    L.msg_create.restype = i
+    L.msg_destroy.argtypes = [vp]
+    L.msg_destroy.restype = None
+    L.msg_last_error.argtypes = [vp]
+    L.msg_last_error.restype = ctypes.c_char_p
+    L.msg_abi_version.argtypes = []
+    L.msg_abi_version.restype = i
+    L.msg_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    L.msg_get_stats.restype = i
+    L.msg_watershed.argtypes = [vp, vp, sz, vp, sz, i, i]
+    L.msg_watershed.restype = i
+    L.msg_colorize.argtypes = [vp, vp, sz, i, i, i, vp, vp, sz]
+    L.msg_colorize.restype = i
+    L.msg_watershed_colorize.argtypes = [vp, vp, sz, vp, sz, i, i, i, vp, vp, sz, vp, sz]
+    L.msg_watershed_colorize.restype = i
+    L.msg_watershed_batch.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
+    L.msg_watershed_batch.restype = i
+    L.msg_watershed_dev.argtypes = [vp, vp, vp, vp, i, i, vp]
+    L.msg_watershed_dev.restype = i
+    L.msg_colorize_dev.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp]
+    L.msg_colorize_dev.restype = i
+    L.msg_watershed_colorize_dev.argtypes = [vp, vp, vp, vp, i, i, i, vp, vp, vp, vp]
+    L.msg_watershed_colorize_dev.restype = i
+    L.msg_edge_weights_dev.argtypes = [vp, vp, vp, vp, i, i, vp]
+    L.msg_edge_weights_dev.restype = i
+    L.msg_set_profiling.argtypes = [vp, i]
+    L.msg_set_profiling.restype = i
+    L.msg_get_kernel_profile.argtypes = [vp, ctypes.POINTER(KernelProfile), i, i]
+    L.msg_get_kernel_profile.restype = i
+    _lib = L
+    return L

@@ -1,0 +1,25 @@
+#!/bin/bash
+# GPU validation pass for gpurun: smoke -> GPU parity tests -> bench -> rocprofv3 kernel stats.
+# Every GPU step has its own time limit; a crash/abort/timeout (rc not in {0,1}) stops the script.
+# usage: scripts/gpu_check.sh <tag> [bench args...]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-run}; shift || true
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 8 "$OUT/$name.log"
+  case $rc in 0|1|5) return 0 ;; *) echo "STOP after $name (rc=$rc)"; exit "$rc" ;; esac
+}
+run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
+run pytest_gpu 900 python -m pytest tests -m gpu -x -q
+run bench 600 python bench.py "$@"
+run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass
+find "$OUT/prof" -name '*stats*' -exec cp {} "$OUT/" \; 2>/dev/null
+echo "== done"

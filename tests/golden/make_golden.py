@@ -1,0 +1,124 @@
+"""Generate the committed golden fixtures for the watershed hot path.
+
+Run from the repo root:  python tests/golden/make_golden.py
+
+Parity is unpinned by the reference (it has no tests or fixtures for this path and OpenCV 3.4.2
+cannot run here), so every expected output below is produced by the C oracle
+(oracle/ws_oracle.c) AND checked against the independent pure-Python restatement
+(oracle/ws_pyref.py) before it is written.  The one real-image case decodes the reference's own
+resource src/main/resources/images/hkp.jpg with PIL (into raw BGR bytes, stored as data) when the
+reference tree is present; the decoded pixels are what the fixture pins, not the JPEG decoder.
+
+Outputs (numpy .npz, no pickles):
+  small_cases.npz  inputs + expected labels + expected colourised/gray outputs, small frames
+  digests.json     SHA-256 of the oracle's label maps for larger synthetic frames
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "opencv-msegment_amd"))
+
+from oracle import ws_oracle, ws_pyref  # noqa: E402
+from msegment import synth  # noqa: E402
+from msegment.jrandom import generate_bgr_palette  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+REF_IMG = "/root/reference/src/main/resources/images/hkp.jpg"
+
+
+def random_markers(rng, H, W, k, lo=-3, hi=6):
+    m = np.zeros((H, W), np.int32)
+    for _ in range(k):
+        m[rng.integers(0, H), rng.integers(0, W)] = rng.integers(lo, hi)
+    return m
+
+
+def cases():
+    rng = np.random.default_rng(20261015)
+    out = []
+    # synthetic generator frames (small sizes of BASELINE configs' kinds)
+    for kind, H, W, seed in [("mosaic", 32, 32, 0), ("mosaic", 48, 64, 5), ("mosaic_noise", 64, 64, 7),
+                             ("random", 40, 48, 9), ("mosaic", 256, 256, 0),
+                             ("mosaic_noise", 96, 80, 11)]:
+        img, m, depth = synth.frame(kind, H, W, seed)
+        out.append(("%s_%dx%d_s%d" % (kind, H, W, seed), img, m, depth))
+    # quantised random images with sparse random markers, negatives and frame labels included
+    for t in range(8):
+        H, W = int(rng.integers(3, 40)), int(rng.integers(3, 40))
+        img = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        if t % 2:
+            img = (img // 85 * 85).astype(np.uint8)
+        m = random_markers(rng, H, W, int(rng.integers(1, 12)))
+        out.append(("rand%d_%dx%d" % (t, H, W), img, m, 5))
+    # a plateau with two seeds (ties everywhere) and a ramp
+    H, W = 24, 30
+    img = np.full((H, W, 3), 77, np.uint8)
+    m = np.zeros((H, W), np.int32)
+    m[5, 5] = 1
+    m[17, 22] = 2
+    out.append(("plateau_24x30", img, m, 2))
+    ramp = np.broadcast_to((np.arange(W, dtype=np.int32) * 7 % 256).astype(np.uint8)[None, :, None], (H, W, 3)).copy()
+    out.append(("ramp_24x30", ramp, m.copy(), 2))
+    # real image from the reference's resources (decoded pixels are the fixture)
+    if os.path.exists(REF_IMG):
+        from PIL import Image
+
+        rgb = np.asarray(Image.open(REF_IMG).convert("RGB"))
+        bgr = np.ascontiguousarray(rgb[:, :, ::-1])
+        H, W, _ = bgr.shape
+        m = synth.seeds(H, W, 4, cells=12)
+        out.append(("hkp_%dx%d" % (H, W), bgr, m, int(m.max())))
+    return out
+
+
+def main():
+    arrays = {}
+    names = []
+    for name, img, m, depth in cases():
+        lab = ws_oracle.watershed(img, m)
+        if img.shape[0] * img.shape[1] <= 70000:
+            ref = ws_pyref.watershed(img, m)
+            assert np.array_equal(lab, ref), "oracle and pyref disagree on %s" % name
+        pal = generate_bgr_palette(depth, 1234)
+        col = ws_oracle.colorize(lab, depth, pal)
+        white = ws_oracle.colorize(lab, depth, None)
+        arrays[name + "__img"] = img
+        arrays[name + "__markers"] = m
+        arrays[name + "__labels"] = lab
+        arrays[name + "__depth"] = np.array(depth, np.int32)
+        arrays[name + "__palette"] = pal
+        arrays[name + "__color"] = col
+        arrays[name + "__white"] = white
+        arrays[name + "__gray"] = ws_oracle.bgr2gray(col)
+        names.append(name)
+    arrays["__names"] = np.array(names)
+    np.savez_compressed(os.path.join(OUT, "small_cases.npz"), **arrays)
+
+    digests = {}
+    for kind, H, W, seed in [("mosaic", 1024, 1024, 1), ("mosaic_noise", 1024, 1024, 1),
+                             ("random", 512, 512, 3), ("mosaic", 4096, 4096, 2)]:
+        img, m, depth = synth.frame(kind, H, W, seed)
+        lab = ws_oracle.watershed(img, m)
+        key = "%s_%dx%d_s%d" % (kind, H, W, seed)
+        digests[key] = {
+            "labels_sha256": hashlib.sha256(lab.tobytes()).hexdigest(),
+            "img_sha256": hashlib.sha256(img.tobytes()).hexdigest(),
+            "markers_sha256": hashlib.sha256(m.tobytes()).hexdigest(),
+            "depth": depth,
+            "wshed_pixels": int((lab == -1).sum()),
+            "zero_pixels": int((lab == 0).sum()),
+        }
+        print(key, digests[key]["labels_sha256"][:16])
+    with open(os.path.join(OUT, "digests.json"), "w") as f:
+        json.dump(digests, f, indent=1, sort_keys=True)
+    print("wrote", len(names), "small cases")
+
+
+if __name__ == "__main__":
+    main()

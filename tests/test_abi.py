@@ -1,0 +1,40 @@
+"""CPU: the C-ABI library loads and exports every symbol include/msegment.h declares.
+No compute calls (there is no GPU in the build container)."""
+import ctypes
+import os
+import re
+
+from msegment import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    hdr = open(os.path.join(ROOT, "include", "msegment.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    return sorted(set(re.findall(r"\b(msg_[a-z_0-9]+)\s*\(", hdr)))
+
+
+def test_library_exports_header_symbols():
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    syms = declared_symbols()
+    assert len(syms) >= 12
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(_lib.EXPORTS)
+
+
+def test_abi_version_and_binding_load():
+    L = _lib.load()
+    assert L.msg_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_null_context_is_rejected_without_gpu():
+    L = _lib.load()
+    assert L.msg_watershed(None, None, 0, None, 0, 4, 4) == _lib.MSG_EINVAL
+    assert L.msg_create(None, 0, 0) == _lib.MSG_EINVAL

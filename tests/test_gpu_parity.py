@@ -1,0 +1,234 @@
+"""GPU parity: libmsegment (HIP, gfx950) vs the CPU oracle, bit-exact on int32 labels and on
+the colourised / gray bytes.  Everything goes through the C ABI (include/msegment.h)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import ws_oracle
+from msegment import synth
+from msegment.jrandom import generate_bgr_palette
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def gpu_ws(seg, img, m):
+    out = np.array(m, dtype=np.int32, copy=True)
+    seg.watershed(img, out)
+    return out
+
+
+def test_kats(seg):
+    img = np.zeros((5, 5, 3), np.uint8)
+    m = np.zeros((5, 5), np.int32)
+    m[1, 1], m[3, 3] = 1, 2
+    want = np.array([[-1, -1, -1, -1, -1], [-1, 1, 1, -1, -1], [-1, 1, -1, 2, -1],
+                     [-1, -1, 2, 2, -1], [-1, -1, -1, -1, -1]], np.int32)
+    assert np.array_equal(gpu_ws(seg, img, m), want)
+    m = np.zeros((3, 3), np.int32)
+    m[0, 0] = 5
+    out = gpu_ws(seg, np.zeros((3, 3, 3), np.uint8), m)
+    assert out[1, 1] == 0 and (out != 0).sum() == 8
+    m = np.zeros((3, 3), np.int32)
+    m[1, 1] = -7
+    assert gpu_ws(seg, np.zeros((3, 3, 3), np.uint8), m)[1, 1] == 0
+    for shape in [(1, 1), (1, 7), (2, 2), (7, 1), (2, 9), (9, 2)]:
+        assert (gpu_ws(seg, np.zeros(shape + (3,), np.uint8), np.ones(shape, np.int32)) == -1).all()
+
+
+def test_empty_frames(seg):
+    for shape in [(0, 0), (0, 5), (5, 0)]:
+        m = np.zeros(shape, np.int32)
+        seg.watershed(np.zeros(shape + (3,), np.uint8), m)
+
+
+def test_golden_small_cases(seg):
+    z = np.load(os.path.join(GOLD, "small_cases.npz"))
+    for n in list(z["__names"]):
+        img, m, d = z[n + "__img"], z[n + "__markers"], int(z[n + "__depth"])
+        work = m.copy()
+        dst, gray = seg.watershed_colorize(img, work, d, z[n + "__palette"], gray=True)
+        assert np.array_equal(work, z[n + "__labels"]), n
+        assert np.array_equal(dst, z[n + "__color"]), n
+        assert np.array_equal(gray, z[n + "__gray"]), n
+        assert np.array_equal(seg.colorize(work, d, None), z[n + "__white"]), n
+
+
+def test_random_small_vs_oracle(seg):
+    rng = np.random.default_rng(7)
+    for t in range(150):
+        H, W = (int(v) for v in rng.integers(1, 48, 2))
+        img = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        q = t % 4
+        if q == 0:
+            img = (img // 128 * 128).astype(np.uint8)
+        elif q == 1:
+            img = (img // 32).astype(np.uint8)
+        elif q == 2:
+            img[:] = img[0, 0]
+        m = np.zeros((H, W), np.int32)
+        for _ in range(int(rng.integers(0, 16))):
+            m[rng.integers(0, H), rng.integers(0, W)] = rng.integers(-4, 7)
+        assert np.array_equal(gpu_ws(seg, img, m), ws_oracle.watershed(img, m)), (t, H, W)
+
+
+def test_dense_and_adjacent_seeds(seg):
+    rng = np.random.default_rng(11)
+    for t in range(20):
+        H, W = 37, 53
+        img = (rng.integers(0, 256, (H, W, 3), dtype=np.uint8) // (64 if t % 2 else 1)).astype(np.uint8)
+        m = rng.integers(-2, 9, (H, W)).astype(np.int32) * (rng.random((H, W)) < 0.3)
+        assert np.array_equal(gpu_ws(seg, img, m.astype(np.int32)), ws_oracle.watershed(img, m)), t
+
+
+def test_strided_views_in_place(seg):
+    img, m, d = synth.frame("mosaic_noise", 70, 90, 5)
+    big_img = np.zeros((70, 100, 3), np.uint8)
+    big_img[:, :90] = img
+    big_m = np.full((70, 97), 12345, np.int32)
+    big_m[:, :90] = m
+    view = big_m[:, :90]
+    seg.watershed(big_img[:, :90], view)
+    assert np.array_equal(view, ws_oracle.watershed(img, m))
+    assert (big_m[:, 90:] == 12345).all()
+
+
+@pytest.mark.parametrize("kind,H,W,seed", [("mosaic", 256, 256, 0), ("mosaic_noise", 256, 256, 3),
+                                           ("random", 192, 160, 4), ("mosaic_noise", 333, 517, 8)])
+def test_synthetic_vs_oracle(seg, kind, H, W, seed):
+    img, m, d = synth.frame(kind, H, W, seed)
+    assert np.array_equal(gpu_ws(seg, img, m), ws_oracle.watershed(img, m))
+
+
+def test_config2_1024_mosaic_digest(seg):
+    dg = json.load(open(os.path.join(GOLD, "digests.json")))["mosaic_1024x1024_s1"]
+    img, m, d = synth.frame("mosaic", 1024, 1024, 1)
+    out = gpu_ws(seg, img, m)
+    assert hashlib.sha256(out.tobytes()).hexdigest() == dg["labels_sha256"]
+
+
+def test_config3_4096_mosaic_digest_and_properties(seg):
+    dg = json.load(open(os.path.join(GOLD, "digests.json")))["mosaic_4096x4096_s2"]
+    img, m, d = synth.frame("mosaic", 4096, 4096, 2)
+    out = gpu_ws(seg, img, m)
+    assert hashlib.sha256(out.tobytes()).hexdigest() == dg["labels_sha256"]
+    check_properties(m, out)
+
+
+def check_properties(m, out):
+    """Size-independent watershed invariants."""
+    H, W = m.shape
+    assert (out[0] == -1).all() and (out[-1] == -1).all() and (out[:, 0] == -1).all() and (out[:, -1] == -1).all()
+    seeds = set(np.unique(m[1:-1, 1:-1][m[1:-1, 1:-1] > 0]).tolist())
+    labs = set(np.unique(out[out > 0]).tolist())
+    assert labs <= seeds
+    inner = m[1:-1, 1:-1] > 0
+    assert np.array_equal(out[1:-1, 1:-1][inner], m[1:-1, 1:-1][inner])  # seeds never change
+    # two 4-adjacent pixels with different positive labels are both input seeds
+    for a, b, sa, sb in [(out[:, :-1], out[:, 1:], m[:, :-1], m[:, 1:]), (out[:-1], out[1:], m[:-1], m[1:])]:
+        bad = (a > 0) & (b > 0) & (a != b)
+        assert ((sa[bad] > 0) & (sb[bad] > 0)).all()
+    assert not (out == -2).any()
+
+
+def test_noise_1024_vs_oracle(seg):
+    img, m, d = synth.frame("mosaic_noise", 1024, 1024, 1)
+    out = gpu_ws(seg, img, m)
+    dg = json.load(open(os.path.join(GOLD, "digests.json")))["mosaic_noise_1024x1024_s1"]
+    assert hashlib.sha256(out.tobytes()).hexdigest() == dg["labels_sha256"]
+
+
+def test_repeated_calls_same_context(seg):
+    img, m, d = synth.frame("mosaic_noise", 128, 128, 2)
+    want = ws_oracle.watershed(img, m)
+    for _ in range(5):
+        assert np.array_equal(gpu_ws(seg, img, m), want)
+    # a bigger frame then a smaller one (workspace reuse)
+    img2, m2, _ = synth.frame("mosaic", 600, 400, 9)
+    assert np.array_equal(gpu_ws(seg, img2, m2), ws_oracle.watershed(img2, m2))
+    assert np.array_equal(gpu_ws(seg, img, m), want)
+
+
+def test_batch_api(seg):
+    frames = [synth.frame("mosaic_noise", 64 + 8 * k, 80, 100 + k)[:2] for k in range(4)]
+    work = [(img, m.copy()) for img, m in frames]
+    seg.watershed_batch(work)
+    for (img, m), (_, out) in zip(frames, work):
+        assert np.array_equal(out, ws_oracle.watershed(img, m))
+
+
+def test_colorize_palette_sizes(seg):
+    rng = np.random.default_rng(3)
+    for depth in [0, 1, 7, 5000, 20000, 70000]:
+        lab = rng.integers(-2, depth + 3, (61, 77)).astype(np.int32)
+        pal = generate_bgr_palette(depth, depth + 1)
+        assert np.array_equal(seg.colorize(lab, depth, pal), ws_oracle.colorize(lab, depth, pal)), depth
+        assert np.array_equal(seg.colorize(lab, depth, None), ws_oracle.colorize(lab, depth, None)), depth
+
+
+def test_invalid_arguments(seg):
+    import msegment
+
+    with pytest.raises(msegment.MsegError):
+        seg.watershed(np.zeros((4, 4, 3), np.uint8), np.zeros((4, 5), np.int32))
+    with pytest.raises(msegment.MsegError):
+        seg.watershed(np.zeros((4, 4), np.uint8), np.zeros((4, 4), np.int32))
+    with pytest.raises(msegment.MsegError):
+        seg.watershed(np.zeros((4, 4, 3), np.uint8), np.zeros((4, 4), np.float32))
+
+
+def test_device_api_torch(seg):
+    import torch
+
+    img, m, d = synth.frame("mosaic_noise", 300, 260, 6)
+    pal = generate_bgr_palette(d, 5)
+    dev = torch.device("cuda", seg.device)
+    t_img = torch.from_numpy(img).to(dev)
+    t_m = torch.from_numpy(m).to(dev)
+    t_lab = torch.empty_like(t_m)
+    t_pal = torch.from_numpy(pal).to(dev)
+    t_dst = torch.empty((300, 260, 3), dtype=torch.uint8, device=dev)
+    t_gray = torch.empty((300, 260), dtype=torch.uint8, device=dev)
+    seg.watershed_colorize_dev(t_img, t_m, t_lab, d, t_pal, t_dst, t_gray)
+    torch.cuda.synchronize()
+    want = ws_oracle.watershed(img, m)
+    assert np.array_equal(t_lab.cpu().numpy(), want)
+    assert np.array_equal(t_m.cpu().numpy(), m)  # out-of-place: input untouched
+    col = ws_oracle.colorize(want, d, pal)
+    assert np.array_equal(t_dst.cpu().numpy(), col)
+    assert np.array_equal(t_gray.cpu().numpy(), ws_oracle.bgr2gray(col))
+
+
+def test_edge_weights_dev(seg):
+    import torch
+
+    img = synth.random_image(123, 77, 1)
+    dev = torch.device("cuda", seg.device)
+    t = torch.from_numpy(img).to(dev)
+    wr = torch.empty((123, 77), dtype=torch.uint8, device=dev)
+    wd = torch.empty_like(wr)
+    seg.edge_weights_dev(t, wr, wd)
+    torch.cuda.synchronize()
+    x = img.astype(np.int32)
+    er = np.zeros((123, 77), np.uint8)
+    ed = np.zeros((123, 77), np.uint8)
+    er[:, :-1] = np.abs(x[:, 1:] - x[:, :-1]).max(axis=2)
+    ed[:-1] = np.abs(x[1:] - x[:-1]).max(axis=2)
+    assert np.array_equal(wr.cpu().numpy(), er) and np.array_equal(wd.cpu().numpy(), ed)
+
+
+def test_picture_service_mirror(seg):
+    import msegment
+
+    img, m, d = synth.frame("mosaic", 128, 96, 12)
+    ps = msegment.PictureService(segmenter=seg, seed=99)
+    work = m.copy()
+    dst = ps.watershed(img, work, d, True)
+    want = ws_oracle.watershed(img, m)
+    assert np.array_equal(work, want)
+    assert np.array_equal(dst, ws_oracle.colorize(want, d, generate_bgr_palette(d, 99)))
+    work = m.copy()
+    assert np.array_equal(ps.watershed(img, work, d, False), ws_oracle.colorize(want, d, None))
