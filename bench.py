@@ -69,6 +69,12 @@ def reduce_max(x, device=None):
     return float(t.item())
 
 
+def whole_job_mpx(world, npx, steps, dt_max):
+    """Whole-job throughput: every rank segments `steps` frames of `npx` pixels; the job takes
+    the slowest rank's time."""
+    return world * npx * steps / dt_max / 1e6
+
+
 def kernel_roofline(prof, stats_per_step, npx, steps):
     """Pick the kernel with the largest total time; achieved = algorithmic bytes per launch /
     average launch duration (both from the same HIP-event-timed steps)."""
@@ -166,7 +172,7 @@ def main(argv=None):
 
     dt = timed_steps(step, args.steps, barrier, sync)
     dt_max = reduce_max(dt, dev)
-    value = world * S * S * args.steps / dt_max / 1e6
+    value = whole_job_mpx(world, S * S, args.steps, dt_max)
     ms_per_step = 1000.0 * dt_max / args.steps
     log("[rank %d] %.3f ms/step (max over ranks %.3f)" % (rank, 1000 * dt / args.steps, ms_per_step))
 

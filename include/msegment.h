@@ -51,9 +51,12 @@ typedef struct msg_stats {
     int64_t rows, cols;     /* size of the last frame                                        */
     int64_t items;          /* batch items resolved, committed or not (>= pops)               */
     int64_t pushes;         /* queue appends after phase 1                                    */
+    int64_t diag[8];        /* msg_set_diag counters (0 when off): k_resolve gather cycles,
+                               dependency-loop cycles, loop rounds, max loop cycles, wave-rounds;
+                               k_small loop rounds, k_small launches that worked; reserved      */
 } msg_stats;
 
-#define MSG_NKERNELS 8
+#define MSG_NKERNELS 10
 typedef struct msg_kernel_profile {
     char    name[32];       /* kernel name, e.g. "k_resolve"                                   */
     int64_t launches;       /* launches timed since the last reset                              */
@@ -73,6 +76,9 @@ int  msg_get_stats(const msg_ctx* ctx, msg_stats* out);
  * to max_entries records and returns how many; reset != 0 zeroes the totals. */
 int  msg_set_profiling(msg_ctx* ctx, int enable);
 int  msg_get_kernel_profile(msg_ctx* ctx, msg_kernel_profile* out, int max_entries, int reset);
+/* In-kernel cycle counters (s_memtime) for the flood kernels, reported in msg_stats.diag.
+ * Diagnostics only: they add atomics to the kernels; never enabled in timed runs. */
+int  msg_set_diag(msg_ctx* ctx, int enable);
 
 /* ---- host-buffer entry points (synchronous; strides in BYTES) ---------------------------- */
 

@@ -29,10 +29,11 @@ struct msg_ctx {
   Ctl* d_ctl = nullptr;
   // flood workspace (sized for cap_n pixels)
   long long cap_n = 0;
-  uint8_t *d_wr = nullptr, *d_wd = nullptr, *d_lv1 = nullptr;
-  int32_t *d_qpos = nullptr, *d_qbuf = nullptr, *d_ilist = nullptr;
+  uint32_t* d_w4 = nullptr;
+  uint8_t* d_lv1 = nullptr;
+  int32_t *d_qbuf = nullptr, *d_ilist = nullptr;
   int32_t *d_cnt = nullptr, *d_coff = nullptr, *d_tot = nullptr, *d_choff = nullptr;
-  unsigned long long *d_tl = nullptr, *d_desc = nullptr;
+  unsigned long long *d_tl = nullptr, *d_desc = nullptr, *d_claim = nullptr;
   long long qcap = 0;
   // staging for the host-buffer entry points
   long long stage_n = 0;
@@ -50,6 +51,8 @@ struct msg_ctx {
   msg_stats stats{};
   // optional per-kernel HIP-event profiling (msg_set_profiling)
   bool prof = false;
+  unsigned long long* d_diag = nullptr;  // 8 counters when diagnostics are on
+  bool diag = false;
   std::vector<hipEvent_t> evpool;
   size_t evused = 0;
   std::vector<std::pair<int, size_t>> recs;  // (kernel id, index of the start event)
@@ -60,10 +63,10 @@ struct msg_ctx {
 namespace {
 
 enum KernelId { KID_PREP, KID_INIT_SCAN, KID_COMPACT, KID_RESOLVE, KID_SCAN, KID_SCATTER,
-                KID_COLORIZE, KID_EDGE };
+                KID_COLORIZE, KID_EDGE, KID_SMALL, KID_CLAIM };
 const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_compact", "k_resolve",
                                                 "k_scan", "k_scatter", "k_colorize",
-                                                "k_edge_weights"};
+                                                "k_edge_weights", "k_small", "k_claim"};
 
 hipEvent_t pool_event(msg_ctx* c) {
   if (c->evused == c->evpool.size()) {
@@ -129,10 +132,10 @@ void dfree(T*& p) {
 }
 
 void free_flood(msg_ctx* c) {
-  dfree(c->d_wr); dfree(c->d_wd); dfree(c->d_lv1);
-  dfree(c->d_qpos); dfree(c->d_qbuf); dfree(c->d_ilist);
+  dfree(c->d_w4); dfree(c->d_lv1);
+  dfree(c->d_qbuf); dfree(c->d_ilist);
   dfree(c->d_cnt); dfree(c->d_coff); dfree(c->d_tot); dfree(c->d_choff);
-  dfree(c->d_tl); dfree(c->d_desc);
+  dfree(c->d_tl); dfree(c->d_desc); dfree(c->d_claim);
   c->cap_n = 0;
   c->qcap = 0;
 }
@@ -147,10 +150,8 @@ int ensure_flood(msg_ctx* c, long long N) {
   free_flood(c);
   const long long nch = (N + CH - 1) / CH;
   const long long qcap = 4 * N + 16;
-  HIPCHK(c, hipMalloc((void**)&c->d_wr, N));
-  HIPCHK(c, hipMalloc((void**)&c->d_wd, N));
+  HIPCHK(c, hipMalloc((void**)&c->d_w4, N * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_lv1, N));
-  HIPCHK(c, hipMalloc((void**)&c->d_qpos, N * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_ilist, N * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_qbuf, qcap * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_tl, N * 8));
@@ -159,7 +160,9 @@ int ensure_flood(msg_ctx* c, long long N) {
   HIPCHK(c, hipMalloc((void**)&c->d_coff, nch * NQ * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_tot, nch * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_choff, nch * 4));
+  HIPCHK(c, hipMalloc((void**)&c->d_claim, N * 8));
   HIPCHK(c, hipMemset(c->d_tl, 0, N * 8));
+  HIPCHK(c, hipMemset(c->d_claim, 0, N * 8));
   c->epoch = 1;
   c->cap_n = N;
   c->qcap = qcap;
@@ -179,7 +182,7 @@ int ensure_stage(msg_ctx* c, long long N) {
 
 int check_size(msg_ctx* c, int rows, int cols) {
   if (rows < 0 || cols < 0) return fail(c, MSG_EINVAL, "negative size %d x %d", rows, cols);
-  if ((long long)rows * cols >= 0x7fffffffll / 4)
+  if ((long long)rows * cols > (1ll << 29))
     return fail(c, MSG_EINVAL, "frame too large for one context: %d x %d", rows, cols);
   return MSG_OK;
 }
@@ -196,24 +199,25 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   if (rc) return rc;
   if (c->epoch > 0xF0000000u) {
     HIPCHK(c, hipMemsetAsync(c->d_tl, 0, c->cap_n * 8, st));
+    HIPCHK(c, hipMemsetAsync(c->d_claim, 0, c->cap_n * 8, st));
     c->epoch = 1;
   }
   Ws ws;
   ws.img = d_img;
   ws.mk = d_mk;
-  ws.wr = c->d_wr;
-  ws.wd = c->d_wd;
+  ws.w4 = c->d_w4;
   ws.lv1 = c->d_lv1;
-  ws.qpos = c->d_qpos;
   ws.qbuf = c->d_qbuf;
   ws.ilist = c->d_ilist;
   ws.tl = c->d_tl;
   ws.desc = c->d_desc;
+  ws.claim = c->d_claim;
   ws.cnt = c->d_cnt;
   ws.coff = c->d_coff;
   ws.tot = c->d_tot;
   ws.choff = c->d_choff;
   ws.ctl = c->d_ctl;
+  ws.diag = c->diag ? c->d_diag : nullptr;
   ws.H = H;
   ws.W = W;
   ws.N = N;
@@ -223,21 +227,24 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   const int gres = std::min(npx, RES_GRID_MAX);
   const int gsc = std::min(npx, 1024);
   HIPCHK(c, hipMemsetAsync(c->d_ctl, 0, sizeof(Ctl), st));
+  if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 8 * sizeof(unsigned long long), st));
+  HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)npx * NQ * sizeof(int32_t), st));
   LAUNCH(c, KID_PREP, st, k_prep, dim3(npx), dim3(BS), 0, ws, d_mk_in);
   LAUNCH(c, KID_INIT_SCAN, st, k_init_scan, dim3(1), dim3(1024), 0, ws, npx, c->epoch);
   LAUNCH(c, KID_COMPACT, st, k_compact, dim3(npx), dim3(BS), 0, ws);
-  LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws, 1);
-  LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(BS), 0, ws, 1);
+  LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
+  LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws);
   HIPCHK(c, hipGetLastError());
 
   int it = 0, slot = 0, prev = -1;
   long long syncs = 0;
   for (;;) {
     for (int g = 0; g < c->group; ++g, ++it) {
-      const int par = it & 1;
-      LAUNCH(c, KID_RESOLVE, st, k_resolve, dim3(gres), dim3(BS), 0, ws, par);
-      LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws, par);
-      LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(BS), 0, ws, par);
+      LAUNCH(c, KID_SMALL, st, k_small, dim3(1), dim3(1024), 0, ws);
+      LAUNCH(c, KID_RESOLVE, st, k_resolve, dim3(gres), dim3(BS), 0, ws);
+      LAUNCH(c, KID_CLAIM, st, k_claim, dim3(gres), dim3(BS), 0, ws);
+      LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
+      LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws);
     }
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(c->h_flags + 4 * slot, &c->d_ctl->done, 2 * sizeof(int),
@@ -253,6 +260,8 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   }
   Ctl tail;
   HIPCHK(c, hipMemcpyAsync(&tail, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
+  unsigned long long dgv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c->diag) HIPCHK(c, hipMemcpyAsync(dgv, c->d_diag, sizeof(dgv), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
   ++syncs;
   if (c->prof) collect_profile(c);
@@ -260,6 +269,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   c->stats.pops = tail.pops;
   c->stats.items = tail.items;
   c->stats.pushes = tail.pushes;
+  for (int k = 0; k < 8; ++k) c->stats.diag[k] = (int64_t)dgv[k];
   c->stats.host_syncs = syncs;
   c->epoch += (unsigned)std::min<long long>(tail.batches + 4, 0x7fffffff);
   if (tail.error & ERR_TIMEOUT)
@@ -329,6 +339,7 @@ void msg_destroy(msg_ctx* c) {
   free_stage(c);
   dfree(c->d_pal);
   dfree(c->d_ctl);
+  dfree(c->d_diag);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
@@ -348,6 +359,16 @@ int msg_get_stats(const msg_ctx* c, msg_stats* out) {
 int msg_set_profiling(msg_ctx* c, int enable) {
   if (!c) return MSG_EINVAL;
   c->prof = enable != 0;
+  return MSG_OK;
+}
+
+int msg_set_diag(msg_ctx* c, int enable) {
+  if (!c) return MSG_EINVAL;
+  if (enable && !c->d_diag) {
+    HIPCHK(c, hipSetDevice(c->dev));
+    HIPCHK(c, hipMalloc((void**)&c->d_diag, 8 * sizeof(unsigned long long)));
+  }
+  c->diag = enable != 0;
   return MSG_OK;
 }
 

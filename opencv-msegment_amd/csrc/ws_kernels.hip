@@ -93,8 +93,9 @@ __global__ __launch_bounds__(BS) void k_prep(Ws ws, const int32_t* mk_in) {
     const uint8_t* ip = ws.img + p * 3;
     const int wright = (c + 1 < W) ? cdiff3(ip, ip + 3) : 0;
     const int wdown = (r + 1 < H) ? cdiff3(ip, ip + 3 * (long long)W) : 0;
-    ws.wr[p] = (uint8_t)wright;
-    ws.wd[p] = (uint8_t)wdown;
+    const int wl = (c >= 1) ? cdiff3(ip, ip - 3) : 0;
+    const int wu = (r >= 1) ? cdiff3(ip, ip - 3 * (long long)W) : 0;
+    ws.w4[p] = (uint32_t)wl | ((uint32_t)wright << 8) | ((uint32_t)wu << 16) | ((uint32_t)wdown << 24);
     int32_t out;
     if (r == 0 || r == H - 1 || c == 0 || c == W - 1) {
       out = WSHED;
@@ -104,8 +105,8 @@ __global__ __launch_bounds__(BS) void k_prep(Ws ws, const int32_t* mk_in) {
         out = m;
       } else {
         // interior neighbours (the frame is WSHED in the serial code and never counts)
-        const int wleft = (c >= 2) ? cdiff3(ip, ip - 3) : -1;
-        const int wup = (r >= 2) ? cdiff3(ip, ip - 3 * (long long)W) : -1;
+        const int wleft = (c >= 2) ? wl : -1;
+        const int wup = (r >= 2) ? wu : -1;
         const int wr_i = (c <= W - 3) ? wright : -1;
         const int wd_i = (r <= H - 3) ? wdown : -1;
         int lvl = 256;
@@ -159,50 +160,52 @@ __device__ void column_scan(const int* cnt, int* coff, int nch, const int* parti
   __syncthreads();
 }
 
-__device__ int column_total(int lv_total) {
+__device__ int block_sum(int v) {
   __shared__ int acc;
   if (threadIdx.x == 0) acc = 0;
   __syncthreads();
-  if (lv_total) atomicAdd(&acc, lv_total);
+  if (v) atomicAdd(&acc, v);
   __syncthreads();
-  return acc;
+  const int r = acc;
+  __syncthreads();
+  return r;
 }
 
-// Pick the lowest non-empty bucket as the next batch (or finish).  1024 threads, after tails
-// are final.  Writes bat[nxt].
-__device__ void choose_next(Ctl* ctl, int nxt, unsigned epoch) {
+// The lowest non-empty bucket (or NQ), from head/tail arrays (global or LDS).  Block-wide.
+__device__ int lowest_bucket(const int* head, const int* tail) {
   __shared__ int lmin;
-  const int tid = threadIdx.x;
-  if (tid == 0) lmin = NQ;
+  if (threadIdx.x == 0) lmin = NQ;
   __syncthreads();
-  if (tid < NQ && ctl->qhead[tid] < ctl->qtail[tid]) atomicMin(&lmin, tid);
+  if (threadIdx.x < NQ && head[threadIdx.x] < tail[threadIdx.x]) atomicMin(&lmin, (int)threadIdx.x);
   __syncthreads();
-  if (tid == 0) {
-    Batch nb;
-    nb.mode = 0;
-    nb.epoch = epoch;
-    nb.ncommit = 0;
-    nb.nchunk = 0;
-    if (lmin < NQ) {
-      nb.L = lmin;
-      nb.bstart = ctl->qbase[lmin] + ctl->qhead[lmin];
-      nb.n = ctl->qtail[lmin] - ctl->qhead[lmin];
-      ctl->batches += 1;
-    } else {
-      nb.L = -1;
-      nb.bstart = 0;
-      nb.n = 0;
-      ctl->done = 1;
-    }
-    ctl->bat[nxt] = nb;
-    ctl->cut[nxt] = NONE;
+  const int r = lmin;
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ Batch make_batch(int l, const int* qbase, const int* head, const int* tail,
+                                            unsigned epoch) {
+  Batch nb;
+  nb.mode = 0;
+  nb.epoch = epoch;
+  nb.ncommit = 0;
+  nb.nchunk = 0;
+  nb.pad = 0;
+  if (l < NQ) {
+    nb.L = l;
+    nb.bstart = qbase[l] + head[l];
+    nb.n = tail[l] - head[l];
+  } else {
+    nb.L = -1;
+    nb.bstart = 0;
+    nb.n = 0;
   }
-  __syncthreads();
+  return nb;
 }
 
 // ---------------------------------------------------------------------------------------------
 // Init scan (1 block x 1024): bucket bases from the capacity histogram; exclusive scan of the
-// per-chunk phase-1 counts (compaction offsets); sets up the phase-1 pseudo-batch in bat[1].
+// per-chunk phase-1 counts (compaction offsets); sets up the phase-1 pseudo-batch.
 __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigned epoch0) {
   Ctl* ctl = ws.ctl;
   const int tid = threadIdx.x;
@@ -217,12 +220,10 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
     ctl->qbase[NQ] = (int)min(acc, (long long)0x7fffffff);
     if (acc > ws.qcap) ctl->error = ERR_CAPACITY;
   }
-  // exclusive scan of tot[0..npxchunk) -> choff, 1024 threads, contiguous per-thread ranges
   const int per = (npxchunk + 1023) / 1024;
   const int a = min(npxchunk, tid * per), b = min(npxchunk, a + per);
   long long s = 0;
   for (int c = a; c < b; ++c) s += ws.tot[c];
-  // block exclusive scan of s
   const int lane = tid & 63, wv = tid >> 6;
   long long x = s;
   for (int o = 1; o < 64; o <<= 1) {
@@ -247,9 +248,6 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
     off += ws.tot[c];
   }
   const long long M = total_items;
-  // zero the level histograms of the pseudo-batch's item chunks
-  const long long nch = (M + CH - 1) / CH;
-  for (long long k = tid; k < nch * NQ; k += blockDim.x) ws.cnt[k] = 0;
   if (tid == 0) {
     Batch pb;
     pb.mode = 1;
@@ -258,13 +256,10 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
     pb.n = (int)M;
     pb.epoch = epoch0;
     pb.ncommit = (int)M;
-    pb.nchunk = (int)nch;
-    ctl->bat[1] = pb;
-    ctl->cut[1] = NONE;
-    Batch z = pb;
-    z.mode = 0;
-    z.n = 0;
-    ctl->bat[0] = z;
+    pb.nchunk = (int)((M + CH - 1) / CH);
+    pb.pad = 0;
+    ctl->bat = pb;
+    ctl->cut = NONE;
     if (M == 0) ctl->done = 1;
   }
 }
@@ -274,7 +269,7 @@ __global__ __launch_bounds__(BS) void k_compact(Ws ws) {
   __shared__ int wt[BS / 64];
   __shared__ int run;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-  if (ws.ctl->bat[1].n == 0) return;
+  if (ws.ctl->bat.n == 0 || ws.ctl->bat.mode != 1) return;
   if (tid == 0) run = 0;
   const long long c0 = (long long)blockIdx.x * CH;
   const int base = ws.choff[blockIdx.x];
@@ -300,185 +295,332 @@ __global__ __launch_bounds__(BS) void k_compact(Ws ws) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Resolve one batch: labels (fold of settled + earlier-batch neighbours) and push decisions.
-// Deadlock-free bounded spinning: an item only waits on strictly lower ranks, all blocks of the
-// grid are co-resident (grid <= RES_GRID_MAX), each block walks its chunks in increasing order,
-// and each wave resolves its lanes cooperatively (intra-wave dependencies via shuffles).
-__global__ __launch_bounds__(BS) void k_resolve(Ws ws, int par) {
+// One batch item, everything that does not change while the batch is resolved.  dep[0..3]: rank
+// of an EARLIER batch item adjacent to p in direction d (label dependencies); dep[4+3d+k]: ranks
+// of earlier batch items adjacent to p's d-neighbour n when n is a 0-pixel (an earlier non-WSHED
+// one pushes n first).  -1 = none.  Fully unrolled: registers only.
+struct Item {
+  long long p;
+  int base_lab;      // fold of the settled (>0) neighbours: 0, a label, or WSHED
+  unsigned zero_mask;
+  unsigned wts;      // 4 packed 8-bit edge weights, directions L,R,T,B
+  int dep[16];
+};
+
+__device__ __forceinline__ int fold_lab(int lab, int v) {
+  return (lab == 0) ? v : (lab == v ? v : WSHED);
+}
+
+__device__ __forceinline__ void gather_item(const Ws& ws, int bstart, int i, Item& it) {
+  const long long W = ws.W;
+  const long long p = ws.qbuf[bstart + i];
+  it.p = p;
+  it.base_lab = 0;
+  it.zero_mask = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) it.dep[k] = -1;
+  it.wts = ws.w4[p];
+  const long long nb[4] = {p - 1, p + 1, p - W, p + W};
+  int v[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) v[d] = ws.mk[nb[d]];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if (v[d] > 0) {
+      it.base_lab = fold_lab(it.base_lab, v[d]);
+    } else if (v[d] <= -3) {
+      const int r = state_slot(v[d]) - bstart;
+      if (r >= 0 && r < i) it.dep[d] = r;
+    } else if (v[d] == 0) {
+      it.zero_mask |= 1u << d;
+    }
+  }
+  if (it.base_lab == WSHED) return;  // WSHED absorbs: no label or push dependency matters
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if (!((it.zero_mask >> d) & 1u)) continue;
+    const long long n = nb[d];
+    // n's neighbours other than p (p is n's opposite-direction neighbour)
+    const long long o0 = (d == 0) ? n - 1 : (d == 1) ? n + 1 : n - 1;
+    const long long o1 = (d <= 1) ? n - W : n + 1;
+    const long long o2 = (d == 0 || d == 1) ? n + W : (d == 2) ? n - W : n + W;
+    const long long o[3] = {o0, o1, o2};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int vo = ws.mk[o[k]];
+      if (vo <= -3) {
+        const int r = state_slot(vo) - bstart;
+        if (r >= 0 && r < i) it.dep[4 + 3 * d + k] = r;
+      }
+    }
+  }
+}
+
+// Try to decide the item.  fetch(slot, rank) -> resolved label of an earlier item, 0 = not yet.
+// Decides as early as the known values allow (WSHED absorbs; one earlier non-WSHED claimant
+// decides a lost push).
+template <class F>
+__device__ __forceinline__ bool attempt_item(const Item& it, F fetch, int& lab_out, unsigned& mask_out) {
+  int lab = it.base_lab;
+  bool unknown = false;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int r = it.dep[d];
+    if (r >= 0) {
+      const int v = fetch(d, r);
+      if (v == 0) unknown = true;
+      else if (v > 0) lab = fold_lab(lab, v);
+    }
+  }
+  if (lab == WSHED) {
+    lab_out = WSHED;
+    mask_out = 0;
+    return true;
+  }
+  if (unknown) return false;
+  unsigned m = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if (!((it.zero_mask >> d) & 1u)) continue;
+    bool lose = false, undecided = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int r = it.dep[4 + 3 * d + k];
+      if (r >= 0) {
+        const int v = fetch(4 + 3 * d + k, r);
+        if (v > 0) lose = true;
+        else if (v == 0) undecided = true;
+      }
+    }
+    if (!lose) {
+      if (undecided) return false;
+      m |= 1u << d;
+    }
+  }
+  lab_out = lab;
+  mask_out = m;
+  return true;
+}
+
+__device__ __forceinline__ long long nb_of(long long p, int d, long long W) {
+  return (d == 0) ? p - 1 : (d == 1) ? p + 1 : (d == 2) ? p - W : p + W;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Large batches: labels in k_resolve, push decisions in k_claim.
+//
+// k_resolve: label of every item = fold of its settled neighbours and of the labels of EARLIER
+// batch items adjacent to it (the only intra-batch dependency left: rare, usually in-wave).
+// Ranks are dealt round-robin over the whole grid (block-round r covers ranks
+// [r*G*BS, (r+1)*G*BS)), so a lower rank is in the same round (a co-resident block: grid <=
+// RES_GRID_MAX) or an earlier one: bounded spinning cannot deadlock.  In-wave dependencies go
+// through register shuffles, others through 8-byte {epoch, label} granules.  A non-WSHED item then
+// CLAIMS each 0-neighbour with atomicMax({epoch, ~rank}): the surviving claim is the smallest rank
+// among the non-WSHED items adjacent to that pixel -- serially the first one to push it.
+struct LItem {
+  long long p;
+  int base_lab;
+  unsigned zero_mask;
+  unsigned wts;
+  int ldep[4];
+};
+
+__device__ __forceinline__ void gather_label(const Ws& ws, int bstart, int i, LItem& it) {
+  const long long W = ws.W;
+  const long long p = ws.qbuf[bstart + i];
+  it.p = p;
+  it.base_lab = 0;
+  it.zero_mask = 0;
+  it.wts = ws.w4[p];
+  const long long nb[4] = {p - 1, p + 1, p - W, p + W};
+  int v[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) v[d] = ws.mk[nb[d]];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    it.ldep[d] = -1;
+    if (v[d] > 0) {
+      it.base_lab = fold_lab(it.base_lab, v[d]);
+    } else if (v[d] <= -3) {
+      const int r = state_slot(v[d]) - bstart;
+      if (r >= 0 && r < i) it.ldep[d] = r;
+    } else if (v[d] == 0) {
+      it.zero_mask |= 1u << d;
+    }
+  }
+}
+
+__device__ __forceinline__ unsigned long long claim_tag(unsigned epoch, int rank) {
+  return ((unsigned long long)epoch << 32) | (unsigned long long)(0xffffffffu - (unsigned)rank);
+}
+
+__global__ __launch_bounds__(BS) void k_resolve(Ws ws) {
   Ctl* ctl = ws.ctl;
-  const Batch B = ctl->bat[par];
-  if (B.n == 0 || ctl->error) return;
-  __shared__ int hist[NQ];
+  const Batch B = ctl->bat;
+  if (B.n == 0 || B.mode != 0 || ctl->error) return;
   const int tid = threadIdx.x, lane = lane_id();
-  const int W = ws.W;
-  const int nch = (B.n + CH - 1) / CH;
   const unsigned long long etag = (unsigned long long)B.epoch << 32;
-  for (int ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+  const long long W = ws.W;
+  unsigned long long* const dg = ws.diag;
+  for (int base = blockIdx.x * BS; base < B.n; base += gridDim.x * BS) {
+    const int wbase = base + (tid & ~63);
+    const int i = wbase + lane;
+    const bool valid = i < B.n;
+    const unsigned long long t_a = dg ? __builtin_amdgcn_s_memtime() : 0;
+    long long iters = 0;
+    LItem it;
+    if (valid) {
+      gather_label(ws, B.bstart, i, it);
+    } else {
+      it.p = 0;
+      it.base_lab = WSHED;
+      it.zero_mask = 0;
+      it.wts = 0;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) it.ldep[d] = -1;
+    }
+    unsigned inw_slots = 0;  // wave-uniform: which dependency slots point inside this wave
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      if (__any((unsigned)(it.ldep[d] - wbase) < 64u)) inw_slots |= 1u << d;
+    const bool any_dep = __any(it.ldep[0] >= 0 || it.ldep[1] >= 0 || it.ldep[2] >= 0 || it.ldep[3] >= 0);
+    bool pending = valid;
+    int mylab = 0;
+    long long t0 = 0;
+    int spins = 0;
+    const unsigned long long t_b = dg ? __builtin_amdgcn_s_memtime() : 0;
+    for (;;) {
+      int snap[4] = {0, 0, 0, 0};
+      if (any_dep) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          if ((inw_slots >> d) & 1u) {
+            const int r = it.ldep[d];
+            snap[d] = __shfl(mylab, ((unsigned)(r - wbase) < 64u) ? r - wbase : lane);
+          }
+      }
+      if (pending) {
+        int lab = it.base_lab;
+        bool unknown = false;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int r = it.ldep[d];
+          if (r < 0) continue;
+          int v;
+          if ((unsigned)(r - wbase) < 64u) {
+            v = snap[d];
+          } else {
+            const unsigned long long g = ld_granule(&ws.tl[r]);
+            v = ((g & 0xffffffff00000000ull) == etag) ? (int)(uint32_t)g : 0;
+          }
+          if (v == 0) unknown = true;
+          else if (v > 0) lab = fold_lab(lab, v);
+        }
+        if (lab == WSHED || !unknown) {
+          if (lab == 0) {  // impossible for an exact queue: flag, label as WSHED
+            atomicOr(&ctl->error, ERR_STATE);
+            lab = WSHED;
+          }
+          mylab = lab;
+          st_granule(&ws.tl[i], etag | (uint32_t)lab);
+          const unsigned zm = (lab == WSHED) ? 0u : it.zero_mask;
+          ws.desc[i] = ((unsigned long long)zm << 32) | it.wts;
+          const unsigned long long ct = claim_tag(B.epoch, i);
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+            if ((zm >> d) & 1u) atomicMax(&ws.claim[nb_of(it.p, d, W)], ct);
+          pending = false;
+        }
+      }
+      ++iters;
+      if (!__any(pending)) break;
+      if (++spins > 16) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__hip_atomic_load(&ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+        const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+        if (t0 == 0) t0 = now;
+        else if (now - t0 > SPIN_LIMIT_TICKS) {
+          if (pending) atomicOr(&ctl->error, ERR_TIMEOUT);
+          break;
+        }
+      }
+    }
+    if (dg && lane == 0) {  // diagnostics path only (msg_set_diag)
+      const unsigned long long t_c = __builtin_amdgcn_s_memtime();
+      atomicAdd(&dg[0], t_b - t_a);
+      atomicAdd(&dg[1], t_c - t_b);
+      atomicAdd(&dg[2], (unsigned long long)iters);
+      atomicMax(&dg[3], t_c - t_b);
+      atomicAdd(&dg[4], 1ull);
+    }
+  }
+}
+
+// k_claim: push decisions from the surviving claims, per-chunk level histograms (one global
+// atomic per block-round and level) and the interrupt cut.  No waiting: all claims of the batch
+// were made before this kernel started.
+__global__ __launch_bounds__(BS) void k_claim(Ws ws) {
+  Ctl* ctl = ws.ctl;
+  const Batch B = ctl->bat;
+  if (B.n == 0 || B.mode != 0 || ctl->error) return;
+  __shared__ int hist[NQ];
+  const int tid = threadIdx.x;
+  const long long W = ws.W;
+  for (int base = blockIdx.x * BS; base < B.n; base += gridDim.x * BS) {
     hist[tid] = 0;
     __syncthreads();
-    for (int s = 0; s < SUB; ++s) {
-      const int wbase = ch * CH + s * BS + (tid & ~63);
-      if (wbase >= B.n) break;  // wave-uniform
-      const int i = wbase + lane;
-      const bool valid = i < B.n;
-      // ---- gather phase: everything that does not change during this launch ----
-      long long p = 0;
-      int base_lab = 0;
-      int ldep[4] = {-1, -1, -1, -1};
-      int pdep[4][3];
-      unsigned zero_mask = 0;
-      unsigned wts = 0;  // 4 packed push levels
-      for (int d = 0; d < 4; ++d) pdep[d][0] = pdep[d][1] = pdep[d][2] = -1;
-      if (valid) {
-        p = ws.qbuf[B.bstart + i];
-        const long long nb[4] = {p - 1, p + 1, p - W, p + W};
-        wts = (unsigned)ws.wr[p - 1] | ((unsigned)ws.wr[p] << 8) | ((unsigned)ws.wd[p - W] << 16) |
-              ((unsigned)ws.wd[p] << 24);
-        for (int d = 0; d < 4; ++d) {
-          const int v = ws.mk[nb[d]];
-          if (v > 0) {
-            base_lab = (base_lab == 0) ? v : (base_lab == v ? v : WSHED);
-          } else if (v == INQ) {
-            const int r = ws.qpos[nb[d]] - B.bstart;
-            if (r >= 0 && r < i) ldep[d] = r;
-          } else if (v == 0) {
-            zero_mask |= 1u << d;
-            // neighbours of the 0-pixel other than p: earlier batch items would push it first
-            const long long n = nb[d];
-            const long long nn[4] = {n - 1, n + 1, n - W, n + W};
-            int k = 0;
-            for (int e = 0; e < 4; ++e) {
-              if (nn[e] == p) continue;
-              const int vm = ws.mk[nn[e]];
-              if (vm == INQ) {
-                const int r = ws.qpos[nn[e]] - B.bstart;
-                if (r >= 0 && r < i) pdep[d][k] = r;
-              }
-              ++k;
-            }
-          }
-        }
-      }
-      // ---- cooperative resolution loop ----
-      bool pending = valid;
-      int mylab = 0;  // resolved label (0 = not yet)
-      unsigned mask = 0;
-      long long t0 = 0;
-      int spins = 0;
-      for (;;) {
-        // snapshot of in-wave resolved labels for every dependency slot (uniform shuffles)
-        int lv_in[4], pv_in[4][3];
-        for (int d = 0; d < 4; ++d) {
-          const int r = ldep[d];
-          const bool inw = r >= wbase && r < wbase + 64;
-          lv_in[d] = __shfl(mylab, inw ? r - wbase : lane);
-          for (int k = 0; k < 3; ++k) {
-            const int rr = pdep[d][k];
-            const bool inw2 = rr >= wbase && rr < wbase + 64;
-            pv_in[d][k] = __shfl(mylab, inw2 ? rr - wbase : lane);
-          }
-        }
-        if (pending) {
-          bool ok = true;
-          int lab = base_lab;
-          for (int d = 0; d < 4 && ok; ++d) {
-            const int r = ldep[d];
-            if (r < 0) continue;
-            int v;
-            if (r >= wbase && r < wbase + 64) {
-              v = lv_in[d];
-            } else {
-              const unsigned long long g = ld_granule(&ws.tl[r]);
-              v = ((g & 0xffffffff00000000ull) == etag) ? (int)(uint32_t)g : 0;
-            }
-            if (v == 0) { ok = false; break; }
-            if (v > 0) lab = (lab == 0) ? v : (lab == v ? v : WSHED);
-          }
-          unsigned m = 0;
-          if (ok && lab != WSHED) {
-            for (int d = 0; d < 4 && ok; ++d) {
-              if (!((zero_mask >> d) & 1u)) continue;
-              bool win = true, undecided = false;
-              for (int k = 0; k < 3; ++k) {
-                const int rr = pdep[d][k];
-                if (rr < 0) continue;
-                int v;
-                if (rr >= wbase && rr < wbase + 64) {
-                  v = pv_in[d][k];
-                } else {
-                  const unsigned long long g = ld_granule(&ws.tl[rr]);
-                  v = ((g & 0xffffffff00000000ull) == etag) ? (int)(uint32_t)g : 0;
-                }
-                if (v > 0) { win = false; break; }
-                if (v == 0) undecided = true;
-              }
-              if (win && undecided) ok = false;
-              else if (win) m |= 1u << d;
-            }
-          }
-          if (ok) {
-            if (lab == 0) {  // impossible for an exact queue: flag, label as WSHED
-              atomicOr(&ctl->error, ERR_STATE);
-              lab = WSHED;
-            }
-            mylab = lab;
-            mask = (lab == WSHED) ? 0u : m;
-            st_granule(&ws.tl[i], etag | (uint32_t)lab);
-            ws.desc[i] = ((unsigned long long)mask << 32) | wts;
-            pending = false;
-          }
-        }
-        if (!__any(pending)) break;
-        if (++spins > 32) {
-          __builtin_amdgcn_s_sleep(1);
-          if (__hip_atomic_load(&ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-          const long long now = (long long)__builtin_amdgcn_s_memrealtime();
-          if (t0 == 0) t0 = now;
-          else if (now - t0 > SPIN_LIMIT_TICKS) {
-            if (pending) atomicOr(&ctl->error, ERR_TIMEOUT);
-            break;
-          }
-        }
-      }
-      // histogram + interrupt cut
-      if (valid && mask) {
+    const int i = base + tid;
+    if (i < B.n) {
+      const unsigned long long d = ws.desc[i];
+      const unsigned zm = (unsigned)(d >> 32) & 15u;
+      if (zm) {
+        const unsigned wts = (unsigned)d;
+        const long long p = ws.qbuf[B.bstart + i];
+        const unsigned long long ct = claim_tag(B.epoch, i);
+        unsigned push = 0;
         bool lower = false;
-        for (int d = 0; d < 4; ++d) {
-          if ((mask >> d) & 1u) {
-            const int lv = (wts >> (8 * d)) & 255;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!((zm >> k) & 1u)) continue;
+          if (ws.claim[nb_of(p, k, W)] == ct) {
+            push |= 1u << k;
+            const int lv = (wts >> (8 * k)) & 255;
             atomicAdd(&hist[lv], 1);
             if (lv < B.L) lower = true;
           }
         }
-        if (lower) atomicMin(&ctl->cut[par], i);
+        ws.desc[i] = ((unsigned long long)push << 32) | wts;
+        if (lower) atomicMin(&ctl->cut, i);
       }
     }
     __syncthreads();
-    ws.cnt[(long long)ch * NQ + tid] = hist[tid];
+    if (hist[tid]) atomicAdd(&ws.cnt[(long long)(base / CH) * NQ + tid], hist[tid]);
     __syncthreads();
   }
 }
 
+
 // ---------------------------------------------------------------------------------------------
 // Scan (1 block x 1024): committed prefix, recount of the cut chunk, column scan -> per-chunk
-// bucket offsets, head/tail update, choice of the next batch.
-__global__ __launch_bounds__(1024) void k_scan(Ws ws, int par) {
+// bucket offsets, head/tail update, hand the committed batch to k_scatter (cbat), choose the next.
+__global__ __launch_bounds__(1024) void k_scan(Ws ws) {
   Ctl* ctl = ws.ctl;
-  const Batch B = ctl->bat[par];
-  if (B.n == 0) return;
-  __shared__ int partial[NQ];
+  const Batch B = ctl->bat;
   const int tid = threadIdx.x;
-  if (ctl->error) {  // stop the flood: nothing may be scattered from unresolved descriptors
+  if (B.n == 0 || ctl->error) {  // nothing committed this iteration (finished, or stopped)
     __syncthreads();
     if (tid == 0) {
-      ctl->bat[par].nchunk = 0;
-      ctl->bat[par].ncommit = 0;
-      ctl->bat[par ^ 1].n = 0;
-      ctl->done = 1;
+      ctl->cbat.n = 0;
+      ctl->cbat.nchunk = 0;
+      if (ctl->error) {
+        ctl->bat.n = 0;
+        ctl->done = 1;
+      }
     }
     return;
   }
-  const int cut = ctl->cut[par];
+  __shared__ int partial[NQ];
+  const int cut = ctl->cut;
   const int ncommit = (B.mode == 1 || cut == NONE) ? B.n : cut + 1;
   const int nch = (ncommit + CH - 1) / CH;
   const bool haspartial = (ncommit % CH) != 0 && ncommit != B.n;
@@ -495,7 +637,7 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws, int par) {
   }
   const int oldt = (tid < NQ) ? ctl->qtail[tid] : 0;
   column_scan(ws.cnt, ws.coff, nch, haspartial ? partial : nullptr, ctl->qtail);
-  const int npush = column_total((tid < NQ) ? ctl->qtail[tid] - oldt : 0);
+  const int npush = block_sum((tid < NQ) ? ctl->qtail[tid] - oldt : 0);
   if (tid == 0) {
     ctl->pushes += npush;
     if (B.mode == 0) {
@@ -503,12 +645,22 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws, int par) {
       ctl->pops += ncommit;
       ctl->items += B.n;
     }
-    ctl->bat[par].ncommit = ncommit;
-    ctl->bat[par].nchunk = nch;
-    if (ctl->qbase[NQ] < 0) ctl->error |= ERR_CAPACITY;
+    Batch cb = B;
+    cb.ncommit = ncommit;
+    cb.nchunk = nch;
+    ctl->cbat = cb;
   }
+  // every histogram row this batch accumulated into is consumed: zero it for the next batch
+  const long long rows = (long long)((B.n + CH - 1) / CH) * NQ;
+  for (long long k = tid; k < rows; k += blockDim.x) ws.cnt[k] = 0;
   __syncthreads();
-  choose_next(ctl, par ^ 1, B.epoch + 1);
+  const int l = lowest_bucket(ctl->qhead, ctl->qtail);
+  if (tid == 0) {
+    ctl->bat = make_batch(l, ctl->qbase, ctl->qhead, ctl->qtail, B.epoch + 1);
+    ctl->cut = NONE;
+    if (l < NQ) ctl->batches += 1;
+    else ctl->done = 1;
+  }
 }
 
 // Stable rank of this lane's pushes among the wave's pushes of the same level, in (lane, dir)
@@ -524,16 +676,19 @@ __device__ __forceinline__ void wave_rank(unsigned mask, unsigned lvls, int pos[
     const int myl = rem ? (int)((lvls >> (8 * (__ffs(rem) - 1))) & 255u) : -1;
     const int lsel = __shfl(myl, leader);
     unsigned sel = 0;
+#pragma unroll
     for (int d = 0; d < 4; ++d)
       if (((rem >> d) & 1u) && (int)((lvls >> (8 * d)) & 255u) == lsel) sel |= 1u << d;
     const int cnt = __popc(sel);
     int x = cnt;
+#pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const int y = __shfl_up(x, o);
       if (lane >= o) x += y;
     }
     const int total = __shfl(x, 63);
     int k = x - cnt;
+#pragma unroll
     for (int d = 0; d < 4; ++d)
       if ((sel >> d) & 1u) pos[d] = k++;
     if (lane == 0) wrow[lsel] = total;
@@ -541,25 +696,30 @@ __device__ __forceinline__ void wave_rank(unsigned mask, unsigned lvls, int pos[
   }
 }
 
+
 // Ordered scatter: commit labels of the committed prefix and append its pushes to the buckets in
 // exact (rank, dir) order.  mode 1 (phase-1 pseudo-batch): item i is pixel ilist[i] itself.
-__global__ __launch_bounds__(BS) void k_scatter(Ws ws, int par) {
+// 1024 threads = 16 waves: a 4096-item chunk is 4 sub-rounds.
+__global__ __launch_bounds__(1024) void k_scatter(Ws ws) {
   Ctl* ctl = ws.ctl;
-  const Batch B = ctl->bat[par];
-  if (B.n == 0 || ctl->error) return;
+  const Batch B = ctl->cbat;
+  if (B.nchunk == 0 || ctl->error) return;
+  constexpr int NW = 16;
   __shared__ int run[NQ];
-  __shared__ int wcnt[BS / 64][NQ];
+  __shared__ int tot[NQ];
+  __shared__ int wcnt[NW][NQ];
   __shared__ int qb[NQ];
   const int tid = threadIdx.x, wv = tid >> 6;
-  const int W = ws.W;
-  qb[tid] = ctl->qbase[tid];
+  const long long W = ws.W;
+  if (tid < NQ) qb[tid] = ctl->qbase[tid];
   for (int ch = blockIdx.x; ch < B.nchunk; ch += gridDim.x) {
-    run[tid] = ws.coff[(long long)ch * NQ + tid];
-    for (int k = 0; k < BS / 64; ++k) wcnt[k][tid] = 0;
+    if (tid < NQ) {
+      run[tid] = ws.coff[(long long)ch * NQ + tid];
+#pragma unroll
+      for (int k = 0; k < NW; ++k) wcnt[k][tid] = 0;
+    }
     __syncthreads();
-    for (int s = 0; s < SUB; ++s) {
-      const int i0 = ch * CH + s * BS;
-      if (i0 >= B.ncommit) break;  // block-uniform
+    for (int i0 = ch * CH; i0 < min(ch * CH + CH, B.ncommit); i0 += 1024) {  // block-uniform
       const int i = i0 + tid;
       const bool valid = i < B.ncommit;
       unsigned mask = 0, lvls = 0;
@@ -578,35 +738,212 @@ __global__ __launch_bounds__(BS) void k_scatter(Ws ws, int par) {
       int pos[4] = {0, 0, 0, 0};
       wave_rank(mask, lvls, pos, wcnt[wv]);
       __syncthreads();
+      if (tid < NQ) {  // exclusive prefix over the waves, per level
+        int acc = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+          const int t = wcnt[k][tid];
+          wcnt[k][tid] = acc;
+          acc += t;
+        }
+        tot[tid] = acc;
+      }
+      __syncthreads();
+#pragma unroll
       for (int d = 0; d < 4; ++d) {
         if (!((mask >> d) & 1u)) continue;
         const int lv = (lvls >> (8 * d)) & 255;
-        int off = run[lv] + pos[d];
-        for (int k = 0; k < wv; ++k) off += wcnt[k][lv];
-        const int dest = qb[lv] + off;
+        const int dest = qb[lv] + run[lv] + wcnt[wv][lv] + pos[d];
         if (dest < 0 || (long long)dest >= ws.qcap) {
           atomicOr(&ctl->error, ERR_CAPACITY);
           continue;
         }
-        long long n;
-        if (B.mode == 0) {
-          n = (d == 0) ? p - 1 : (d == 1) ? p + 1 : (d == 2) ? p - W : p + W;
-          ws.mk[n] = INQ;
-        } else {
-          n = p;
-        }
+        const long long n = (B.mode == 0) ? nb_of(p, d, W) : p;
+        ws.mk[n] = queued_state(dest);
         ws.qbuf[dest] = (int32_t)n;
-        ws.qpos[n] = dest;
       }
       __syncthreads();
-      int t = 0;
-      for (int k = 0; k < BS / 64; ++k) {
-        t += wcnt[k][tid];
-        wcnt[k][tid] = 0;
+      if (tid < NQ) {
+        run[tid] += tot[tid];
+#pragma unroll
+        for (int k = 0; k < NW; ++k) wcnt[k][tid] = 0;
       }
-      run[tid] += t;
       __syncthreads();
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Small batches, one workgroup (16 waves), many batches per launch.  Runs of small batches
+// (boundary levels, interrupt cascades, generation tails) dominate the batch count; here each
+// one costs a few workgroup barriers instead of three kernel boundaries.  Labels of the batch
+// live in LDS, so in-block dependencies need no global hand-off.  Exits (writing the queue
+// state back) when the next batch is larger than SMALL_MAX, the flood is done, or on error.
+__global__ __launch_bounds__(1024) void k_small(Ws ws) {
+  constexpr int NW = 16;
+  Ctl* ctl = ws.ctl;
+  __shared__ int s_lab[SMALL_MAX];
+  __shared__ unsigned long long s_desc[SMALL_MAX];
+  __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ], s_tot[NQ];
+  __shared__ int s_wcnt[NW][NQ];
+  __shared__ int s_cut, s_err;
+  __shared__ Batch s_B;
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const long long W = ws.W;
+  if (tid == 0) {
+    s_B = ctl->bat;
+    s_err = ctl->error;
+  }
+  if (tid < NQ) {
+    s_qbase[tid] = ctl->qbase[tid];
+    s_head[tid] = ctl->qhead[tid];
+    s_tail[tid] = ctl->qtail[tid];
+#pragma unroll
+    for (int k = 0; k < NW; ++k) s_wcnt[k][tid] = 0;
+  }
+  __syncthreads();
+  long long nb_batches = 0, nb_pops = 0, nb_items = 0, nb_push = 0, iters = 0;
+  bool worked = false;
+  for (;;) {
+    const Batch B = s_B;
+    if (B.n == 0 || B.mode != 0 || B.n > SMALL_MAX || s_err) break;
+    worked = true;
+    for (int k = tid; k < B.n; k += 1024) s_lab[k] = 0;
+    if (tid == 0) s_cut = NONE;
+    __syncthreads();
+    // ---- resolve: item i on thread i % 1024, rounds in rank order, labels in LDS ----
+    volatile int* vlab = s_lab;
+    for (int base = 0; base < B.n; base += 1024) {
+      const int i = base + tid;
+      const bool valid = i < B.n;
+      Item it;
+      if (valid) gather_item(ws, B.bstart, i, it);
+      bool pending = valid;
+      long long t0 = 0;
+      int spins = 0;
+      for (;;) {
+        if (pending) {
+          auto fetch = [&](int, int r) -> int { return vlab[r]; };
+          int lab;
+          unsigned m;
+          if (attempt_item(it, fetch, lab, m)) {
+            if (lab == 0) {
+              s_err = ERR_STATE;
+              lab = WSHED;
+            }
+            const unsigned mask = (lab == WSHED) ? 0u : m;
+            s_desc[i] = ((unsigned long long)mask << 32) | it.wts;
+            vlab[i] = lab;
+            pending = false;
+            bool lower = false;
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+              if (((mask >> d) & 1u) && (int)((it.wts >> (8 * d)) & 255u) < B.L) lower = true;
+            if (lower) atomicMin(&s_cut, i);
+          }
+        }
+        ++iters;
+        if (!__any(pending)) break;
+        if (++spins > 64) {
+          __builtin_amdgcn_s_sleep(1);
+          const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+          if (t0 == 0) t0 = now;
+          else if (now - t0 > SPIN_LIMIT_TICKS) {
+            if (pending) s_err = ERR_TIMEOUT;
+            break;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (s_err) break;
+    const int ncommit = (s_cut == NONE) ? B.n : s_cut + 1;
+    // ---- commit + ordered append, 1024 items per sub-round ----
+    int pushed = 0;
+    for (int i0 = 0; i0 < ncommit; i0 += 1024) {
+      const int i = i0 + tid;
+      const bool valid = i < ncommit;
+      unsigned mask = 0, lvls = 0;
+      long long p = 0;
+      if (valid) {
+        const unsigned long long d = s_desc[i];
+        mask = (unsigned)(d >> 32) & 15u;
+        lvls = (unsigned)d;
+        p = ws.qbuf[B.bstart + i];
+        ws.mk[p] = vlab[i];
+      }
+      int pos[4] = {0, 0, 0, 0};
+      wave_rank(mask, lvls, pos, s_wcnt[wv]);
+      __syncthreads();
+      if (tid < NQ) {
+        int acc = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+          const int t = s_wcnt[k][tid];
+          s_wcnt[k][tid] = acc;
+          acc += t;
+        }
+        s_tot[tid] = acc;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        if (!((mask >> d) & 1u)) continue;
+        const int lv = (lvls >> (8 * d)) & 255;
+        const int dest = s_qbase[lv] + s_tail[lv] + s_wcnt[wv][lv] + pos[d];
+        if (dest < 0 || (long long)dest >= ws.qcap) {
+          s_err = ERR_CAPACITY;
+          continue;
+        }
+        const long long n = nb_of(p, d, W);
+        ws.mk[n] = queued_state(dest);
+        ws.qbuf[dest] = (int32_t)n;
+        ++pushed;
+      }
+      __syncthreads();
+      if (tid < NQ) {
+        s_tail[tid] += s_tot[tid];
+#pragma unroll
+        for (int k = 0; k < NW; ++k) s_wcnt[k][tid] = 0;
+      }
+      __syncthreads();
+    }
+    const int npush = block_sum(pushed);
+    if (tid == 0) {
+      s_head[B.L] += ncommit;
+      nb_pops += ncommit;
+      nb_items += B.n;
+      nb_push += npush;
+    }
+    __syncthreads();
+    const int l = lowest_bucket(s_head, s_tail);
+    if (tid == 0) {
+      s_B = make_batch(l, s_qbase, s_head, s_tail, B.epoch + 1);
+      if (l < NQ) ++nb_batches;
+    }
+    __syncthreads();
+  }
+  // write the queue state back for the multi-block kernels
+  if (ws.diag && lane == 0 && iters) atomicAdd(&ws.diag[5], (unsigned long long)iters);
+  if (!worked) {
+    if (tid == 0 && s_err && !ctl->error) ctl->error = s_err;
+    return;
+  }
+  if (ws.diag && tid == 0) atomicAdd(&ws.diag[6], (unsigned long long)nb_batches + 1);
+  __syncthreads();
+  if (tid < NQ) {
+    ctl->qhead[tid] = s_head[tid];
+    ctl->qtail[tid] = s_tail[tid];
+  }
+  if (tid == 0) {
+    ctl->bat = s_B;
+    ctl->cut = NONE;
+    ctl->batches += nb_batches;
+    ctl->pops += nb_pops;
+    ctl->items += nb_items;
+    ctl->pushes += nb_push;
+    if (s_err) ctl->error |= s_err;
+    if (s_B.n == 0 && !s_err) ctl->done = 1;
   }
 }
 

@@ -10,9 +10,14 @@ constexpr int BS = 256;          // threads per block of the chunk kernels
 constexpr int CH = 4096;         // items per chunk of the ordered multi-bucket append
 constexpr int SUB = CH / BS;     // sub-rounds per chunk
 constexpr int WSHED = -1;        // cv::watershed WSHED
-constexpr int INQ = -2;          // cv::watershed IN_QUEUE
+constexpr int INQ = -2;          // cv::watershed IN_QUEUE, before the pixel has a queue slot
+// A queued pixel's state word also carries its queue slot (one random load instead of two):
+// state = -3 - slot  (<= -3).  Slots are < 2^31 - 8 (frames are limited to 2^29 pixels).
+__host__ __device__ inline int queued_state(int slot) { return -3 - slot; }
+__host__ __device__ inline int state_slot(int state) { return -3 - state; }
 constexpr int NONE = 0x7fffffff;
-constexpr int RES_GRID_MAX = 512;  // <= 2 blocks of 256 threads per CU: all co-resident
+constexpr int RES_GRID_MAX = 1024; // <= 4 blocks of 256 threads per CU: all co-resident
+constexpr int SMALL_MAX = 4096;    // batches up to this size run inside the one-workgroup k_small
 constexpr int PAL_LDS_MAX = 16384; // palettes up to this many labels are staged in LDS
 constexpr long long SPIN_LIMIT_TICKS = 200000000ll;  // 2 s of s_memrealtime (100 MHz)
 
@@ -36,8 +41,9 @@ struct Ctl {
   int qhead[NQ];
   int qtail[NQ];
   unsigned cap[NQ];
-  Batch bat[2];
-  int cut[2];
+  Batch bat;    // current batch (written by k_init_scan / k_scan / k_small)
+  Batch cbat;   // batch being committed by k_scatter (written by k_scan)
+  int cut;      // first rank of the current batch that pushes below its level (NONE: none)
   int done;
   int error;
   long long batches;
@@ -48,20 +54,20 @@ struct Ctl {
 
 struct Ws {
   const uint8_t* img;
-  int32_t* mk;
-  uint8_t* wr;
-  uint8_t* wd;
+  int32_t* mk;       // label state; a queued pixel holds queued_state(slot) = -3 - slot
+  uint32_t* w4;      // 4 packed 8-bit L-inf distances to the L,R,T,B neighbours
   uint8_t* lv1;
-  int32_t* qpos;
   int32_t* qbuf;
   int32_t* ilist;
   unsigned long long* tl;
   unsigned long long* desc;
+  unsigned long long* claim;  // per-pixel {epoch, ~rank} push claims (k_resolve -> k_claim)
   int32_t* cnt;
   int32_t* coff;
   int32_t* tot;
   int32_t* choff;
   Ctl* ctl;
+  unsigned long long* diag;  // nullptr = off; else 8 counters (msg_set_diag)
   int H, W;
   long long N;
   long long qcap;

@@ -1,0 +1,52 @@
+// msegment_jni.cpp -- JNI shim over the C ABI of include/msegment.h.
+// Build (where a JDK exists):
+//   g++ -O2 -fPIC -shared -I"$JAVA_HOME/include" -I"$JAVA_HOME/include/linux" -I../../include \
+//       msegment_jni.cpp -L../msegment -lmsegment -Wl,-rpath,'$ORIGIN' -o libmsegment_jni.so
+// Replaces the OpenCV 3.4.2 JNI entry Java_org_opencv_imgproc_Imgproc_watershed_10 reached from
+// PictureService.java:909, plus the per-pixel colorByIndexes loop (PictureService.java:913-936).
+#include <jni.h>
+
+#include "msegment.h"
+
+extern "C" {
+
+JNIEXPORT jlong JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_create(JNIEnv*, jclass,
+                                                                                          jint device) {
+  msg_ctx* c = nullptr;
+  return msg_create(&c, device, 0) == MSG_OK ? reinterpret_cast<jlong>(c) : 0;
+}
+
+JNIEXPORT void JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_destroy(JNIEnv*, jclass,
+                                                                                          jlong ctx) {
+  msg_destroy(reinterpret_cast<msg_ctx*>(ctx));
+}
+
+JNIEXPORT jstring JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_lastError(JNIEnv* env,
+                                                                                               jclass, jlong ctx) {
+  return env->NewStringUTF(msg_last_error(reinterpret_cast<msg_ctx*>(ctx)));
+}
+
+JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_watershedColorize(
+    JNIEnv* env, jclass, jlong ctx, jbyteArray bgr, jintArray markers, jint rows, jint cols, jint depth,
+    jbyteArray palette, jbyteArray dst) {
+  msg_ctx* c = reinterpret_cast<msg_ctx*>(ctx);
+  if (!c) return MSG_EINVAL;
+  // pinned (critical) views: no per-pixel JNI traffic, one H2D/D2H per buffer inside libmsegment
+  jbyte* pb = static_cast<jbyte*>(env->GetPrimitiveArrayCritical(bgr, nullptr));
+  jint* pm = static_cast<jint*>(env->GetPrimitiveArrayCritical(markers, nullptr));
+  jbyte* pd = static_cast<jbyte*>(env->GetPrimitiveArrayCritical(dst, nullptr));
+  jbyte* pp = palette ? static_cast<jbyte*>(env->GetPrimitiveArrayCritical(palette, nullptr)) : nullptr;
+  int rc = MSG_EINVAL;
+  if (pb && pm && pd)
+    rc = msg_watershed_colorize(c, reinterpret_cast<const uint8_t*>(pb), (size_t)cols * 3,
+                                reinterpret_cast<int32_t*>(pm), (size_t)cols * 4, rows, cols, depth,
+                                reinterpret_cast<const uint8_t*>(pp), reinterpret_cast<uint8_t*>(pd),
+                                (size_t)cols * 3, nullptr, 0);
+  if (pp) env->ReleasePrimitiveArrayCritical(palette, pp, JNI_ABORT);
+  if (pd) env->ReleasePrimitiveArrayCritical(dst, pd, 0);
+  if (pm) env->ReleasePrimitiveArrayCritical(markers, pm, 0);
+  if (pb) env->ReleasePrimitiveArrayCritical(bgr, pb, JNI_ABORT);
+  return rc;
+}
+
+}  // extern "C"

@@ -83,7 +83,12 @@ class Segmenter:
     def stats(self):
         s = Stats()
         self._check(self._L.msg_get_stats(self._h, ctypes.byref(s)))
-        return {k: getattr(s, k) for k, _ in Stats._fields_}
+        out = {k: getattr(s, k) for k, _ in Stats._fields_}
+        out["diag"] = list(s.diag)
+        return out
+
+    def set_diag(self, on=True):
+        self._check(self._L.msg_set_diag(self._h, 1 if on else 0))
 
     # -- host buffers (numpy) -------------------------------------------------------------
     def watershed(self, bgr, markers):

@@ -24,7 +24,7 @@ EXPORTS = (
     "msg_create", "msg_destroy", "msg_last_error", "msg_abi_version", "msg_get_stats",
     "msg_watershed", "msg_colorize", "msg_watershed_colorize", "msg_watershed_batch",
     "msg_watershed_dev", "msg_colorize_dev", "msg_watershed_colorize_dev", "msg_edge_weights_dev",
-    "msg_set_profiling", "msg_get_kernel_profile",
+    "msg_set_profiling", "msg_get_kernel_profile", "msg_set_diag",
 )
 
 
@@ -39,14 +39,15 @@ class MsegError(RuntimeError):
 class Stats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_int64), ("pops", ctypes.c_int64),
                 ("host_syncs", ctypes.c_int64), ("rows", ctypes.c_int64), ("cols", ctypes.c_int64),
-                ("items", ctypes.c_int64), ("pushes", ctypes.c_int64)]
+                ("items", ctypes.c_int64), ("pushes", ctypes.c_int64),
+                ("diag", ctypes.c_int64 * 8)]
 
 
 class KernelProfile(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int64), ("total_ms", ctypes.c_double)]
 
 
-NKERNELS = 8
+NKERNELS = 10
 
 
 def build(arch="gfx950"):
@@ -63,6 +64,14 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError("libmsegment.so not built at %s (run __graft_entry__.build())" % LIB_PATH)
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7.  If it is
+    # importable, load it first so libmsegment's DT_NEEDED binds to that same runtime (same
+    # SONAME) and device pointers/streams from torch tensors are valid in both.  Loading ours
+    # first would pull /opt/rocm's copy and torch would later fail with "No HIP GPUs".
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp = ctypes.c_void_p
     sz = ctypes.c_size_t
@@ -95,6 +104,8 @@ def load():
     L.msg_edge_weights_dev.restype = i
     L.msg_set_profiling.argtypes = [vp, i]
     L.msg_set_profiling.restype = i
+    L.msg_set_diag.argtypes = [vp, i]
+    L.msg_set_diag.restype = i
     L.msg_get_kernel_profile.argtypes = [vp, ctypes.POINTER(KernelProfile), i, i]
     L.msg_get_kernel_profile.restype = i
     _lib = L

@@ -20,6 +20,7 @@ run() {
 run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
 run pytest_gpu 900 python -m pytest tests -m gpu -x -q
 run bench 600 python bench.py "$@"
+[ -n "${EXTRA_BENCH:-}" ] && run bench_extra 600 python bench.py $EXTRA_BENCH
 run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass
 find "$OUT/prof" -name '*stats*' -exec cp {} "$OUT/" \; 2>/dev/null
 echo "== done"
