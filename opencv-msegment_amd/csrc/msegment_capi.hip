@@ -212,6 +212,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   ws.tl = c->d_tl;
   ws.desc = c->d_desc;
   ws.claim = c->d_claim;
+  ws.ipx = c->d_ilist;
   ws.cnt = c->d_cnt;
   ws.coff = c->d_coff;
   ws.tot = c->d_tot;

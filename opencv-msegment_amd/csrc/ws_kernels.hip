@@ -171,36 +171,109 @@ __device__ int block_sum(int v) {
   return r;
 }
 
-// The lowest non-empty bucket (or NQ), from head/tail arrays (global or LDS).  Block-wide.
-__device__ int lowest_bucket(const int* head, const int* tail) {
-  __shared__ int lmin;
-  if (threadIdx.x == 0) lmin = NQ;
-  __syncthreads();
-  if (threadIdx.x < NQ && head[threadIdx.x] < tail[threadIdx.x]) atomicMin(&lmin, (int)threadIdx.x);
-  __syncthreads();
-  const int r = lmin;
-  __syncthreads();
-  return r;
+// Next batch from the queue state (global or LDS arrays).  Block-wide, >= 64 threads, wave 0
+// does the work; result in segs[0..*nseg) and *ntot (LDS), visible after the caller's barrier.
+// The batch is the lowest non-empty bucket, extended by the following non-empty buckets (in level
+// order, total <= MERGE_CAP) when `minpush` -- the lowest level the previous batch pushed -- is
+// above that lowest level: a batch that did not feed its own or a lower level is unlikely to
+// start a generation, so later segments are unlikely to be cut (the cut rules keep it exact).
+__device__ void form_batch(const int* qbase, const int* head, const int* tail, int minpush,
+                           Seg* segs, int* nseg_out, int* n_out) {
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  int cnt[4];
+  int ne = 0, sum = 0, lo = NQ;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int l = lane * 4 + k;
+    cnt[k] = tail[l] - head[l];
+    if (cnt[k] > 0) {
+      ++ne;
+      sum += cnt[k];
+      lo = min(lo, l);
+    }
+  }
+  int xe = ne, xs = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int ye = __shfl_up(xe, o), ys = __shfl_up(xs, o);
+    if (lane >= o) {
+      xe += ye;
+      xs += ys;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lo = min(lo, __shfl_xor(lo, o));
+  const bool merge = minpush > lo;
+  int segi = xe - ne, cum = xs - sum, inc_n = 0, inc_items = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (cnt[k] <= 0) continue;
+    const int l = lane * 4 + k;
+    const bool inc = (segi == 0) || (merge && cum + cnt[k] <= MERGE_CAP);
+    if (inc) {
+      Seg s;
+      s.L = l;
+      s.bstart = qbase[l] + head[l];
+      s.rank = cum;
+      s.n = cnt[k];
+      segs[segi] = s;
+      ++inc_n;
+      inc_items += cnt[k];
+    }
+    cum += cnt[k];
+    ++segi;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    inc_n += __shfl_xor(inc_n, o);
+    inc_items += __shfl_xor(inc_items, o);
+  }
+  if (lane == 0) {
+    *nseg_out = inc_n;
+    *n_out = inc_items;
+  }
 }
 
-__device__ __forceinline__ Batch make_batch(int l, const int* qbase, const int* head, const int* tail,
-                                            unsigned epoch) {
-  Batch nb;
-  nb.mode = 0;
-  nb.epoch = epoch;
-  nb.ncommit = 0;
-  nb.nchunk = 0;
-  nb.pad = 0;
-  if (l < NQ) {
-    nb.L = l;
-    nb.bstart = qbase[l] + head[l];
-    nb.n = tail[l] - head[l];
-  } else {
-    nb.L = -1;
-    nb.bstart = 0;
-    nb.n = 0;
+// rank -> segment (segments sorted by rank); slot -> batch rank or -1 (sorted by bstart too:
+// bucket regions are laid out in level order).
+__device__ __forceinline__ int seg_of_rank(const Seg* s, int nseg, int r) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s[mid].rank <= r) lo = mid;
+    else hi = mid - 1;
   }
-  return nb;
+  return lo;
+}
+__device__ __forceinline__ int rank_of_slot(const Seg* s, int nseg, int slot) {
+  if (nseg == 1) {
+    const int r = slot - s[0].bstart;
+    return (r >= 0 && r < s[0].n) ? r : -1;
+  }
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s[mid].bstart <= slot) lo = mid;
+    else hi = mid - 1;
+  }
+  const int off = slot - s[lo].bstart;
+  return (off >= 0 && off < s[lo].n) ? s[lo].rank + off : -1;
+}
+// First segment after `sg` whose level is above t (NONE if none): the batch must end before it
+// when an item of segment sg pushes at level t (those pushes are popped before that bucket).
+__device__ __forceinline__ int seg_cut_for(const Seg* s, int nseg, int sg, int t) {
+  int lo = sg + 1, hi = nseg;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (s[mid].L > t) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo < nseg ? lo : NONE;
+}
+
+__device__ __forceinline__ void load_segs(const Ctl* ctl, const Batch& B, Seg* s) {
+  for (int k = threadIdx.x; k < B.nseg; k += blockDim.x) s[k] = ctl->seg[k];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -254,12 +327,14 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
     pb.L = -1;
     pb.bstart = 0;
     pb.n = (int)M;
+    pb.nseg = 0;
     pb.epoch = epoch0;
     pb.ncommit = (int)M;
     pb.nchunk = (int)((M + CH - 1) / CH);
-    pb.pad = 0;
     ctl->bat = pb;
     ctl->cut = NONE;
+    ctl->segcut = NONE;
+    ctl->minpush = 0;  // the first flood batch is never merged
     if (M == 0) ctl->done = 1;
   }
 }
@@ -286,7 +361,7 @@ __global__ __launch_bounds__(BS) void k_compact(Ws ws) {
       const long long k = (long long)base + off;
       const int lv = ws.lv1[p];
       ws.ilist[k] = (int32_t)p;
-      ws.desc[k] = (1ull << 32) | (unsigned long long)lv;
+      ws.desc[k] = make_desc((unsigned)lv, 1u, 0, 0);
       atomicAdd(&ws.cnt[(k / CH) * NQ + lv], 1);
     }
     __syncthreads();
@@ -294,116 +369,16 @@ __global__ __launch_bounds__(BS) void k_compact(Ws ws) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// One batch item, everything that does not change while the batch is resolved.  dep[0..3]: rank
-// of an EARLIER batch item adjacent to p in direction d (label dependencies); dep[4+3d+k]: ranks
-// of earlier batch items adjacent to p's d-neighbour n when n is a 0-pixel (an earlier non-WSHED
-// one pushes n first).  -1 = none.  Fully unrolled: registers only.
-struct Item {
-  long long p;
-  int base_lab;      // fold of the settled (>0) neighbours: 0, a label, or WSHED
-  unsigned zero_mask;
-  unsigned wts;      // 4 packed 8-bit edge weights, directions L,R,T,B
-  int dep[16];
-};
-
 __device__ __forceinline__ int fold_lab(int lab, int v) {
   return (lab == 0) ? v : (lab == v ? v : WSHED);
 }
 
-__device__ __forceinline__ void gather_item(const Ws& ws, int bstart, int i, Item& it) {
-  const long long W = ws.W;
-  const long long p = ws.qbuf[bstart + i];
-  it.p = p;
-  it.base_lab = 0;
-  it.zero_mask = 0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) it.dep[k] = -1;
-  it.wts = ws.w4[p];
-  const long long nb[4] = {p - 1, p + 1, p - W, p + W};
-  int v[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) v[d] = ws.mk[nb[d]];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    if (v[d] > 0) {
-      it.base_lab = fold_lab(it.base_lab, v[d]);
-    } else if (v[d] <= -3) {
-      const int r = state_slot(v[d]) - bstart;
-      if (r >= 0 && r < i) it.dep[d] = r;
-    } else if (v[d] == 0) {
-      it.zero_mask |= 1u << d;
-    }
-  }
-  if (it.base_lab == WSHED) return;  // WSHED absorbs: no label or push dependency matters
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    if (!((it.zero_mask >> d) & 1u)) continue;
-    const long long n = nb[d];
-    // n's neighbours other than p (p is n's opposite-direction neighbour)
-    const long long o0 = (d == 0) ? n - 1 : (d == 1) ? n + 1 : n - 1;
-    const long long o1 = (d <= 1) ? n - W : n + 1;
-    const long long o2 = (d == 0 || d == 1) ? n + W : (d == 2) ? n - W : n + W;
-    const long long o[3] = {o0, o1, o2};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int vo = ws.mk[o[k]];
-      if (vo <= -3) {
-        const int r = state_slot(vo) - bstart;
-        if (r >= 0 && r < i) it.dep[4 + 3 * d + k] = r;
-      }
-    }
-  }
-}
-
-// Try to decide the item.  fetch(slot, rank) -> resolved label of an earlier item, 0 = not yet.
-// Decides as early as the known values allow (WSHED absorbs; one earlier non-WSHED claimant
-// decides a lost push).
-template <class F>
-__device__ __forceinline__ bool attempt_item(const Item& it, F fetch, int& lab_out, unsigned& mask_out) {
-  int lab = it.base_lab;
-  bool unknown = false;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const int r = it.dep[d];
-    if (r >= 0) {
-      const int v = fetch(d, r);
-      if (v == 0) unknown = true;
-      else if (v > 0) lab = fold_lab(lab, v);
-    }
-  }
-  if (lab == WSHED) {
-    lab_out = WSHED;
-    mask_out = 0;
-    return true;
-  }
-  if (unknown) return false;
-  unsigned m = 0;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    if (!((it.zero_mask >> d) & 1u)) continue;
-    bool lose = false, undecided = false;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int r = it.dep[4 + 3 * d + k];
-      if (r >= 0) {
-        const int v = fetch(4 + 3 * d + k, r);
-        if (v > 0) lose = true;
-        else if (v == 0) undecided = true;
-      }
-    }
-    if (!lose) {
-      if (undecided) return false;
-      m |= 1u << d;
-    }
-  }
-  lab_out = lab;
-  mask_out = m;
-  return true;
-}
-
 __device__ __forceinline__ long long nb_of(long long p, int d, long long W) {
   return (d == 0) ? p - 1 : (d == 1) ? p + 1 : (d == 2) ? p - W : p + W;
+}
+
+__device__ __forceinline__ unsigned long long claim_tag(unsigned epoch, int rank) {
+  return ((unsigned long long)epoch << 32) | (unsigned long long)(0xffffffffu - (unsigned)rank);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -425,9 +400,10 @@ struct LItem {
   int ldep[4];
 };
 
-__device__ __forceinline__ void gather_label(const Ws& ws, int bstart, int i, LItem& it) {
+__device__ __forceinline__ void gather_label(const Ws& ws, const Seg* segs, int nseg, int i, int slot,
+                                             LItem& it) {
   const long long W = ws.W;
-  const long long p = ws.qbuf[bstart + i];
+  const long long p = ws.qbuf[slot];
   it.p = p;
   it.base_lab = 0;
   it.zero_mask = 0;
@@ -442,7 +418,7 @@ __device__ __forceinline__ void gather_label(const Ws& ws, int bstart, int i, LI
     if (v[d] > 0) {
       it.base_lab = fold_lab(it.base_lab, v[d]);
     } else if (v[d] <= -3) {
-      const int r = state_slot(v[d]) - bstart;
+      const int r = rank_of_slot(segs, nseg, state_slot(v[d]));
       if (r >= 0 && r < i) it.ldep[d] = r;
     } else if (v[d] == 0) {
       it.zero_mask |= 1u << d;
@@ -450,14 +426,13 @@ __device__ __forceinline__ void gather_label(const Ws& ws, int bstart, int i, LI
   }
 }
 
-__device__ __forceinline__ unsigned long long claim_tag(unsigned epoch, int rank) {
-  return ((unsigned long long)epoch << 32) | (unsigned long long)(0xffffffffu - (unsigned)rank);
-}
-
 __global__ __launch_bounds__(BS) void k_resolve(Ws ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
   if (B.n == 0 || B.mode != 0 || ctl->error) return;
+  __shared__ Seg segs[NQ];
+  load_segs(ctl, B, segs);
+  __syncthreads();
   const int tid = threadIdx.x, lane = lane_id();
   const unsigned long long etag = (unsigned long long)B.epoch << 32;
   const long long W = ws.W;
@@ -469,8 +444,12 @@ __global__ __launch_bounds__(BS) void k_resolve(Ws ws) {
     const unsigned long long t_a = dg ? __builtin_amdgcn_s_memtime() : 0;
     long long iters = 0;
     LItem it;
+    int sg = 0;
     if (valid) {
-      gather_label(ws, B.bstart, i, it);
+      sg = (B.nseg == 1) ? 0 : seg_of_rank(segs, B.nseg, i);
+      const int slot = segs[sg].bstart + (i - segs[sg].rank);
+      gather_label(ws, segs, B.nseg, i, slot, it);
+      ws.ipx[i] = (int32_t)it.p;
     } else {
       it.p = 0;
       it.base_lab = WSHED;
@@ -524,7 +503,7 @@ __global__ __launch_bounds__(BS) void k_resolve(Ws ws) {
           mylab = lab;
           st_granule(&ws.tl[i], etag | (uint32_t)lab);
           const unsigned zm = (lab == WSHED) ? 0u : it.zero_mask;
-          ws.desc[i] = ((unsigned long long)zm << 32) | it.wts;
+          ws.desc[i] = make_desc(it.wts, zm, segs[sg].L, sg);
           const unsigned long long ct = claim_tag(B.epoch, i);
 #pragma unroll
           for (int d = 0; d < 4; ++d)
@@ -557,13 +536,19 @@ __global__ __launch_bounds__(BS) void k_resolve(Ws ws) {
 }
 
 // k_claim: push decisions from the surviving claims, per-chunk level histograms (one global
-// atomic per block-round and level) and the interrupt cut.  No waiting: all claims of the batch
-// were made before this kernel started.
+// atomic per block-round and level), the interrupt cut (push below the item's own level: cut
+// after the item) and the segment cut (push below a LATER segment's level: end the batch before
+// that segment), and the lowest pushed level.  No waiting: every claim of the batch was made
+// before this kernel started.
 __global__ __launch_bounds__(BS) void k_claim(Ws ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
   if (B.n == 0 || B.mode != 0 || ctl->error) return;
   __shared__ int hist[NQ];
+  __shared__ Seg segs[NQ];
+  __shared__ int s_minpush;
+  load_segs(ctl, B, segs);
+  if (threadIdx.x == 0) s_minpush = NQ;
   const int tid = threadIdx.x;
   const long long W = ws.W;
   for (int base = blockIdx.x * BS; base < B.n; base += gridDim.x * BS) {
@@ -575,10 +560,12 @@ __global__ __launch_bounds__(BS) void k_claim(Ws ws) {
       const unsigned zm = (unsigned)(d >> 32) & 15u;
       if (zm) {
         const unsigned wts = (unsigned)d;
-        const long long p = ws.qbuf[B.bstart + i];
+        const int lvi = (int)((d >> 40) & 255), sg = (int)((d >> 48) & 255);
+        const long long p = ws.ipx[i];
         const unsigned long long ct = claim_tag(B.epoch, i);
         unsigned push = 0;
         bool lower = false;
+        int tmin = NQ;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           if (!((zm >> k) & 1u)) continue;
@@ -586,23 +573,33 @@ __global__ __launch_bounds__(BS) void k_claim(Ws ws) {
             push |= 1u << k;
             const int lv = (wts >> (8 * k)) & 255;
             atomicAdd(&hist[lv], 1);
-            if (lv < B.L) lower = true;
+            if (lv < lvi) lower = true;
+            else tmin = min(tmin, lv);
           }
         }
-        ws.desc[i] = ((unsigned long long)push << 32) | wts;
+        ws.desc[i] = (d & ~(15ull << 32)) | ((unsigned long long)push << 32);
         if (lower) atomicMin(&ctl->cut, i);
+        if (tmin < NQ) {
+          atomicMin(&s_minpush, tmin);
+          if (B.nseg > 1) {
+            const int m = seg_cut_for(segs, B.nseg, sg, tmin);
+            if (m != NONE) atomicMin(&ctl->segcut, m);
+          }
+        }
+        if (lower) atomicMin(&s_minpush, 0);
       }
     }
     __syncthreads();
     if (hist[tid]) atomicAdd(&ws.cnt[(long long)(base / CH) * NQ + tid], hist[tid]);
     __syncthreads();
   }
+  if (tid == 0 && s_minpush < NQ) atomicMin(&ctl->minpush, s_minpush);
 }
 
-
 // ---------------------------------------------------------------------------------------------
-// Scan (1 block x 1024): committed prefix, recount of the cut chunk, column scan -> per-chunk
-// bucket offsets, head/tail update, hand the committed batch to k_scatter (cbat), choose the next.
+// Scan (1 block x 1024): committed prefix (interrupt cut, segment cut), recount of the cut chunk,
+// column scan -> per-chunk bucket offsets, head/tail update, hand the committed batch to k_scatter
+// (cbat), form the next batch.
 __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
@@ -620,8 +617,14 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
     return;
   }
   __shared__ int partial[NQ];
-  const int cut = ctl->cut;
-  const int ncommit = (B.mode == 1 || cut == NONE) ? B.n : cut + 1;
+  __shared__ Seg nsegs[NQ];
+  __shared__ int s_nseg, s_n;
+  int ncommit = B.n;
+  if (B.mode == 0) {
+    const int cut = ctl->cut, segcut = ctl->segcut;
+    if (cut != NONE) ncommit = min(ncommit, cut + 1);
+    if (segcut != NONE) ncommit = min(ncommit, ctl->seg[segcut].rank);
+  }
   const int nch = (ncommit + CH - 1) / CH;
   const bool haspartial = (ncommit % CH) != 0 && ncommit != B.n;
   if (haspartial) {
@@ -638,10 +641,13 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
   const int oldt = (tid < NQ) ? ctl->qtail[tid] : 0;
   column_scan(ws.cnt, ws.coff, nch, haspartial ? partial : nullptr, ctl->qtail);
   const int npush = block_sum((tid < NQ) ? ctl->qtail[tid] - oldt : 0);
+  if (B.mode == 0 && tid < B.nseg) {  // advance every segment's bucket head by what it committed
+    const Seg s = ctl->seg[tid];
+    ctl->qhead[s.L] += max(0, min(ncommit - s.rank, s.n));
+  }
   if (tid == 0) {
     ctl->pushes += npush;
     if (B.mode == 0) {
-      ctl->qhead[B.L] += ncommit;
       ctl->pops += ncommit;
       ctl->items += B.n;
     }
@@ -654,11 +660,25 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
   const long long rows = (long long)((B.n + CH - 1) / CH) * NQ;
   for (long long k = tid; k < rows; k += blockDim.x) ws.cnt[k] = 0;
   __syncthreads();
-  const int l = lowest_bucket(ctl->qhead, ctl->qtail);
+  form_batch(ctl->qbase, ctl->qhead, ctl->qtail, B.mode == 0 ? ctl->minpush : 0, nsegs, &s_nseg, &s_n);
+  __syncthreads();
+  const int ns = s_nseg;
+  for (int k = tid; k < ns; k += blockDim.x) ctl->seg[k] = nsegs[k];
   if (tid == 0) {
-    ctl->bat = make_batch(l, ctl->qbase, ctl->qhead, ctl->qtail, B.epoch + 1);
+    Batch nb;
+    nb.mode = 0;
+    nb.epoch = B.epoch + 1;
+    nb.ncommit = 0;
+    nb.nchunk = 0;
+    nb.nseg = ns;
+    nb.n = (ns > 0) ? s_n : 0;
+    nb.L = (ns > 0) ? nsegs[0].L : -1;
+    nb.bstart = (ns > 0) ? nsegs[0].bstart : 0;
+    ctl->bat = nb;
     ctl->cut = NONE;
-    if (l < NQ) ctl->batches += 1;
+    ctl->segcut = NONE;
+    ctl->minpush = NQ;
+    if (ns > 0) ctl->batches += 1;
     else ctl->done = 1;
   }
 }
@@ -696,7 +716,6 @@ __device__ __forceinline__ void wave_rank(unsigned mask, unsigned lvls, int pos[
   }
 }
 
-
 // Ordered scatter: commit labels of the committed prefix and append its pushes to the buckets in
 // exact (rank, dir) order.  mode 1 (phase-1 pseudo-batch): item i is pixel ilist[i] itself.
 // 1024 threads = 16 waves: a 4096-item chunk is 4 sub-rounds.
@@ -729,7 +748,7 @@ __global__ __launch_bounds__(1024) void k_scatter(Ws ws) {
         mask = (unsigned)(d >> 32) & 15u;
         lvls = (unsigned)d;
         if (B.mode == 0) {
-          p = ws.qbuf[B.bstart + i];
+          p = ws.ipx[i];
           ws.mk[p] = (int32_t)(uint32_t)ws.tl[i];
         } else {
           p = ws.ilist[i];
@@ -775,10 +794,109 @@ __global__ __launch_bounds__(1024) void k_scatter(Ws ws) {
 
 // ---------------------------------------------------------------------------------------------
 // Small batches, one workgroup (16 waves), many batches per launch.  Runs of small batches
-// (boundary levels, interrupt cascades, generation tails) dominate the batch count; here each
-// one costs a few workgroup barriers instead of three kernel boundaries.  Labels of the batch
-// live in LDS, so in-block dependencies need no global hand-off.  Exits (writing the queue
-// state back) when the next batch is larger than SMALL_MAX, the flood is done, or on error.
+// (interrupt cascades, generation tails) dominate the batch count; here each one costs a few
+// workgroup barriers instead of five kernel boundaries.  Labels of the batch live in LDS, so
+// push decisions are pulled directly (an earlier non-WSHED batch item adjacent to the target
+// pushes it first) instead of claimed.  Exits, writing the queue state back, when the next batch
+// is larger than SMALL_MAX, the flood is done, or on error.
+struct Item {
+  long long p;
+  int base_lab;      // fold of the settled (>0) neighbours: 0, a label, or WSHED
+  unsigned zero_mask;
+  unsigned wts;      // 4 packed 8-bit edge weights, directions L,R,T,B
+  int dep[16];       // 0..3 label deps, 4+3d+k push deps (earlier items adjacent to the d-target)
+};
+
+__device__ __forceinline__ void gather_item(const Ws& ws, const Seg* segs, int nseg, int i, int slot,
+                                            Item& it) {
+  const long long W = ws.W;
+  const long long p = ws.qbuf[slot];
+  it.p = p;
+  it.base_lab = 0;
+  it.zero_mask = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) it.dep[k] = -1;
+  it.wts = ws.w4[p];
+  const long long nb[4] = {p - 1, p + 1, p - W, p + W};
+  int v[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) v[d] = ws.mk[nb[d]];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if (v[d] > 0) {
+      it.base_lab = fold_lab(it.base_lab, v[d]);
+    } else if (v[d] <= -3) {
+      const int r = rank_of_slot(segs, nseg, state_slot(v[d]));
+      if (r >= 0 && r < i) it.dep[d] = r;
+    } else if (v[d] == 0) {
+      it.zero_mask |= 1u << d;
+    }
+  }
+  if (it.base_lab == WSHED) return;  // WSHED absorbs: no label or push dependency matters
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if (!((it.zero_mask >> d) & 1u)) continue;
+    const long long n = nb[d];
+    // n's neighbours other than p (p is n's opposite-direction neighbour)
+    const long long o0 = (d == 0) ? n - 1 : (d == 1) ? n + 1 : n - 1;
+    const long long o1 = (d <= 1) ? n - W : n + 1;
+    const long long o2 = (d == 0 || d == 1) ? n + W : (d == 2) ? n - W : n + W;
+    const long long o[3] = {o0, o1, o2};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int vo = ws.mk[o[k]];
+      if (vo <= -3) {
+        const int r = rank_of_slot(segs, nseg, state_slot(vo));
+        if (r >= 0 && r < i) it.dep[4 + 3 * d + k] = r;
+      }
+    }
+  }
+}
+
+// Try to decide the item.  fetch(rank) -> resolved label of an earlier item, 0 = not yet.
+template <class F>
+__device__ __forceinline__ bool attempt_item(const Item& it, F fetch, int& lab_out, unsigned& mask_out) {
+  int lab = it.base_lab;
+  bool unknown = false;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int r = it.dep[d];
+    if (r >= 0) {
+      const int v = fetch(r);
+      if (v == 0) unknown = true;
+      else if (v > 0) lab = fold_lab(lab, v);
+    }
+  }
+  if (lab == WSHED) {
+    lab_out = WSHED;
+    mask_out = 0;
+    return true;
+  }
+  if (unknown) return false;
+  unsigned m = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if (!((it.zero_mask >> d) & 1u)) continue;
+    bool lose = false, undecided = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int r = it.dep[4 + 3 * d + k];
+      if (r >= 0) {
+        const int v = fetch(r);
+        if (v > 0) lose = true;
+        else if (v == 0) undecided = true;
+      }
+    }
+    if (!lose) {
+      if (undecided) return false;
+      m |= 1u << d;
+    }
+  }
+  lab_out = lab;
+  mask_out = m;
+  return true;
+}
+
 __global__ __launch_bounds__(1024) void k_small(Ws ws) {
   constexpr int NW = 16;
   Ctl* ctl = ws.ctl;
@@ -786,7 +904,8 @@ __global__ __launch_bounds__(1024) void k_small(Ws ws) {
   __shared__ unsigned long long s_desc[SMALL_MAX];
   __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ], s_tot[NQ];
   __shared__ int s_wcnt[NW][NQ];
-  __shared__ int s_cut, s_err;
+  __shared__ Seg s_seg[NQ];
+  __shared__ int s_cut, s_segcut, s_minpush, s_err, s_nseg, s_n;
   __shared__ Batch s_B;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const long long W = ws.W;
@@ -800,6 +919,7 @@ __global__ __launch_bounds__(1024) void k_small(Ws ws) {
     s_tail[tid] = ctl->qtail[tid];
 #pragma unroll
     for (int k = 0; k < NW; ++k) s_wcnt[k][tid] = 0;
+    s_seg[tid] = ctl->seg[tid];
   }
   __syncthreads();
   long long nb_batches = 0, nb_pops = 0, nb_items = 0, nb_push = 0, iters = 0;
@@ -809,7 +929,11 @@ __global__ __launch_bounds__(1024) void k_small(Ws ws) {
     if (B.n == 0 || B.mode != 0 || B.n > SMALL_MAX || s_err) break;
     worked = true;
     for (int k = tid; k < B.n; k += 1024) s_lab[k] = 0;
-    if (tid == 0) s_cut = NONE;
+    if (tid == 0) {
+      s_cut = NONE;
+      s_segcut = NONE;
+      s_minpush = NQ;
+    }
     __syncthreads();
     // ---- resolve: item i on thread i % 1024, rounds in rank order, labels in LDS ----
     volatile int* vlab = s_lab;
@@ -817,13 +941,17 @@ __global__ __launch_bounds__(1024) void k_small(Ws ws) {
       const int i = base + tid;
       const bool valid = i < B.n;
       Item it;
-      if (valid) gather_item(ws, B.bstart, i, it);
+      int sg = 0;
+      if (valid) {
+        sg = (B.nseg == 1) ? 0 : seg_of_rank(s_seg, B.nseg, i);
+        gather_item(ws, s_seg, B.nseg, i, s_seg[sg].bstart + (i - s_seg[sg].rank), it);
+      }
       bool pending = valid;
       long long t0 = 0;
       int spins = 0;
       for (;;) {
         if (pending) {
-          auto fetch = [&](int, int r) -> int { return vlab[r]; };
+          auto fetch = [&](int r) -> int { return vlab[r]; };
           int lab;
           unsigned m;
           if (attempt_item(it, fetch, lab, m)) {
@@ -832,14 +960,30 @@ __global__ __launch_bounds__(1024) void k_small(Ws ws) {
               lab = WSHED;
             }
             const unsigned mask = (lab == WSHED) ? 0u : m;
-            s_desc[i] = ((unsigned long long)mask << 32) | it.wts;
+            const int lvi = s_seg[sg].L;
+            s_desc[i] = make_desc(it.wts, mask, lvi, sg);
             vlab[i] = lab;
             pending = false;
             bool lower = false;
+            int tmin = NQ;
 #pragma unroll
-            for (int d = 0; d < 4; ++d)
-              if (((mask >> d) & 1u) && (int)((it.wts >> (8 * d)) & 255u) < B.L) lower = true;
-            if (lower) atomicMin(&s_cut, i);
+            for (int d = 0; d < 4; ++d) {
+              if (!((mask >> d) & 1u)) continue;
+              const int t = (int)((it.wts >> (8 * d)) & 255u);
+              if (t < lvi) lower = true;
+              else tmin = min(tmin, t);
+            }
+            if (lower) {
+              atomicMin(&s_cut, i);
+              atomicMin(&s_minpush, 0);
+            }
+            if (tmin < NQ) {
+              atomicMin(&s_minpush, tmin);
+              if (B.nseg > 1) {
+                const int mseg = seg_cut_for(s_seg, B.nseg, sg, tmin);
+                if (mseg != NONE) atomicMin(&s_segcut, mseg);
+              }
+            }
           }
         }
         ++iters;
@@ -857,7 +1001,9 @@ __global__ __launch_bounds__(1024) void k_small(Ws ws) {
     }
     __syncthreads();
     if (s_err) break;
-    const int ncommit = (s_cut == NONE) ? B.n : s_cut + 1;
+    int ncommit = B.n;
+    if (s_cut != NONE) ncommit = min(ncommit, s_cut + 1);
+    if (s_segcut != NONE) ncommit = min(ncommit, s_seg[s_segcut].rank);
     // ---- commit + ordered append, 1024 items per sub-round ----
     int pushed = 0;
     for (int i0 = 0; i0 < ncommit; i0 += 1024) {
@@ -869,7 +1015,8 @@ __global__ __launch_bounds__(1024) void k_small(Ws ws) {
         const unsigned long long d = s_desc[i];
         mask = (unsigned)(d >> 32) & 15u;
         lvls = (unsigned)d;
-        p = ws.qbuf[B.bstart + i];
+        const int sg = (int)((d >> 48) & 255);
+        p = ws.qbuf[s_seg[sg].bstart + (i - s_seg[sg].rank)];
         ws.mk[p] = vlab[i];
       }
       int pos[4] = {0, 0, 0, 0};
@@ -909,17 +1056,30 @@ __global__ __launch_bounds__(1024) void k_small(Ws ws) {
       __syncthreads();
     }
     const int npush = block_sum(pushed);
+    if (tid < B.nseg) {
+      const Seg s = s_seg[tid];
+      s_head[s.L] += max(0, min(ncommit - s.rank, s.n));
+    }
     if (tid == 0) {
-      s_head[B.L] += ncommit;
       nb_pops += ncommit;
       nb_items += B.n;
       nb_push += npush;
     }
     __syncthreads();
-    const int l = lowest_bucket(s_head, s_tail);
+    form_batch(s_qbase, s_head, s_tail, s_minpush, s_seg, &s_nseg, &s_n);
+    __syncthreads();
     if (tid == 0) {
-      s_B = make_batch(l, s_qbase, s_head, s_tail, B.epoch + 1);
-      if (l < NQ) ++nb_batches;
+      Batch nb;
+      nb.mode = 0;
+      nb.epoch = B.epoch + 1;
+      nb.ncommit = 0;
+      nb.nchunk = 0;
+      nb.nseg = s_nseg;
+      nb.n = (s_nseg > 0) ? s_n : 0;
+      nb.L = (s_nseg > 0) ? s_seg[0].L : -1;
+      nb.bstart = (s_nseg > 0) ? s_seg[0].bstart : 0;
+      s_B = nb;
+      if (s_nseg > 0) ++nb_batches;
     }
     __syncthreads();
   }
@@ -935,9 +1095,12 @@ __global__ __launch_bounds__(1024) void k_small(Ws ws) {
     ctl->qhead[tid] = s_head[tid];
     ctl->qtail[tid] = s_tail[tid];
   }
+  for (int k = tid; k < s_B.nseg; k += 1024) ctl->seg[k] = s_seg[k];
   if (tid == 0) {
     ctl->bat = s_B;
     ctl->cut = NONE;
+    ctl->segcut = NONE;
+    ctl->minpush = NQ;
     ctl->batches += nb_batches;
     ctl->pops += nb_pops;
     ctl->items += nb_items;

@@ -19,21 +19,37 @@ constexpr int NONE = 0x7fffffff;
 constexpr int RES_GRID_MAX = 1024; // <= 4 blocks of 256 threads per CU: all co-resident
 constexpr int SMALL_MAX = 4096;    // batches up to this size run inside the one-workgroup k_small
 constexpr int PAL_LDS_MAX = 16384; // palettes up to this many labels are staged in LDS
+constexpr int MERGE_CAP = 1 << 22; // largest multi-segment batch (items)
 constexpr long long SPIN_LIMIT_TICKS = 200000000ll;  // 2 s of s_memrealtime (100 MHz)
 
 constexpr int ERR_TIMEOUT = 1;
 constexpr int ERR_STATE = 2;
 constexpr int ERR_CAPACITY = 4;
 
+// desc word of a batch item: bits 0-31 the 4 edge weights, 32-35 push (or 0-neighbour) mask,
+// 40-47 the item's level, 48-55 its segment.
+__host__ __device__ inline unsigned long long make_desc(unsigned wts, unsigned mask, int lv, int sg) {
+  return (unsigned long long)wts | ((unsigned long long)mask << 32) | ((unsigned long long)lv << 40) |
+         ((unsigned long long)sg << 48);
+}
+
+// One segment of a batch: the current contents of bucket L, ranks [rank, rank + n).
+struct Seg {
+  int L;
+  int bstart;      // absolute qbuf slot of the segment's first item
+  int rank;        // batch rank of that item
+  int n;
+};
+
 struct Batch {
-  int L;           // bucket level (-1 for the phase-1 pseudo-batch)
+  int L;           // level of the first segment (-1 for the phase-1 pseudo-batch)
   int bstart;      // absolute qbuf slot of rank 0
-  int n;           // items in the batch (0 = nothing to do / finished)
+  int n;           // items in the batch, all segments (0 = nothing to do / finished)
+  int nseg;        // segments (consecutive non-empty buckets in level order)
   unsigned epoch;  // tag of this batch's tl granules
   int ncommit;     // committed prefix (set by k_scan)
   int nchunk;      // chunks of the committed prefix (set by k_scan)
   int mode;        // 0 = flood batch, 1 = phase-1 pseudo-batch (items = ilist)
-  int pad;
 };
 
 struct Ctl {
@@ -43,7 +59,10 @@ struct Ctl {
   unsigned cap[NQ];
   Batch bat;    // current batch (written by k_init_scan / k_scan / k_small)
   Batch cbat;   // batch being committed by k_scatter (written by k_scan)
-  int cut;      // first rank of the current batch that pushes below its level (NONE: none)
+  Seg seg[NQ];  // segments of the current batch
+  int cut;      // first rank of the current batch that pushes below its own level (NONE: none)
+  int segcut;   // first segment invalidated by a push below its level (NONE: none)
+  int minpush;  // lowest level pushed by the current batch (merge heuristic)
   int done;
   int error;
   long long batches;
@@ -62,6 +81,7 @@ struct Ws {
   unsigned long long* tl;
   unsigned long long* desc;
   unsigned long long* claim;  // per-pixel {epoch, ~rank} push claims (k_resolve -> k_claim)
+  int32_t* ipx;      // pixel of each rank of the current batch (k_resolve -> k_claim, k_scatter)
   int32_t* cnt;
   int32_t* coff;
   int32_t* tot;
