@@ -187,6 +187,18 @@ def main(argv=None):
         seg.set_profiling(False)
         kern = kernel_roofline(prof, st, S * S, args.steps)
 
+    pcie = None
+    if rank == 0 and world == 1:
+        # host-buffer entry point (what the JNI shim calls): H2D + flood + colourise + D2H
+        reps, t_host = 3, 0.0
+        for _ in range(reps):
+            work = m.copy()
+            t1 = time.perf_counter()
+            seg.watershed_colorize(img, work, depth, None)
+            t_host += time.perf_counter() - t1
+        pcie = {"value": round(S * S * reps / t_host / 1e6, 3), "unit": "Mpx/s",
+                "note": "msg_watershed_colorize on pageable host buffers, %d frames" % reps}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, cpu_lab = cpu_baseline(img, m, depth)
@@ -216,6 +228,7 @@ def main(argv=None):
                        "frames_per_rank_per_step": 1, "parallelism": "replicas%d (no collectives)" % world},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "pcie_inclusive": pcie,
             "e2e_hbm": {"achieved": round(e2e_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(e2e_gbs / HBM_PEAK_GBS, 5), "bytes_per_pixel": E2E_BYTES_PER_PIXEL},
             "flood": {"batches": st["batches"], "pops": st["pops"], "items": st["items"],
