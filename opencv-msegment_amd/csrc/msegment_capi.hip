@@ -48,6 +48,7 @@ struct msg_ctx {
   hipEvent_t ev[2] = {nullptr, nullptr};
   unsigned epoch = 1;
   int group = 8;
+  int res_grid = 0;   // co-resident k_resolve blocks (occupancy x CUs), bounded-spin safety
   msg_stats stats{};
   // optional per-kernel HIP-event profiling (msg_set_profiling)
   bool prof = false;
@@ -225,7 +226,8 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   ws.qcap = c->qcap;
 
   const int npx = (int)((N + CH - 1) / CH);
-  const int gres = std::min(npx, RES_GRID_MAX);
+  const int gres = std::max(1, std::min(c->res_grid, (int)((N + RBS - 1) / RBS)));
+  const int gclaim = std::min(npx * (CH / BS), 1024);
   const int gsc = std::min(npx, 1024);
   HIPCHK(c, hipMemsetAsync(c->d_ctl, 0, sizeof(Ctl), st));
   if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 8 * sizeof(unsigned long long), st));
@@ -238,23 +240,30 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   HIPCHK(c, hipGetLastError());
 
   int it = 0, slot = 0, prev = -1;
+  c->group = 4;
   long long syncs = 0;
   for (;;) {
     for (int g = 0; g < c->group; ++g, ++it) {
-      LAUNCH(c, KID_SMALL, st, k_small, dim3(1), dim3(1024), 0, ws);
-      LAUNCH(c, KID_RESOLVE, st, k_resolve, dim3(gres), dim3(BS), 0, ws);
-      LAUNCH(c, KID_CLAIM, st, k_claim, dim3(gres), dim3(BS), 0, ws);
+      LAUNCH(c, KID_RESOLVE, st, k_resolve, dim3(gres), dim3(RBS), 0, ws);
+      LAUNCH(c, KID_CLAIM, st, k_claim, dim3(gclaim), dim3(BS), 0, ws);
       LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
       LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws);
     }
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipMemcpyAsync(c->h_flags + 4 * slot, &c->d_ctl->done, 2 * sizeof(int),
+    static_assert(offsetof(Ctl, error) == offsetof(Ctl, done) + sizeof(int) &&
+                      offsetof(Ctl, remaining) == offsetof(Ctl, done) + 2 * sizeof(int),
+                  "polled control words must be contiguous");
+    HIPCHK(c, hipMemcpyAsync(c->h_flags + 4 * slot, &c->d_ctl->done, 3 * sizeof(int),
                              hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipEventRecord(c->ev[slot], st));
     if (prev >= 0) {
       HIPCHK(c, hipEventSynchronize(c->ev[prev]));
       ++syncs;
       if (c->h_flags[4 * prev] || c->h_flags[4 * prev + 1]) break;
+      // fewer queued items -> fewer batches left: shrink the group so that the iterations
+      // enqueued past the end of the flood (no-ops, but each still a launch) stay few
+      const int rem = c->h_flags[4 * prev + 2];
+      c->group = rem > (1 << 20) ? 8 : rem > (1 << 17) ? 4 : rem > (1 << 14) ? 2 : 1;
     }
     prev = slot;
     slot ^= 1;
@@ -327,6 +336,18 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
       hipEventCreateWithFlags(&c->ev[1], hipEventDisableTiming) != hipSuccess) {
     msg_destroy(c);
     return MSG_EHIP;
+  }
+  {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_resolve, RBS, 0) != hipSuccess || cus <= 0 ||
+        per <= 0) {
+      msg_destroy(c);
+      return MSG_EHIP;
+    }
+    // one 1024-thread block per CU (k_resolve is VGPR-limited to 16 waves/CU); never trust a
+    // larger occupancy answer for a grid whose blocks wait on each other
+    c->res_grid = cus * std::min(per, 1);
   }
   *out = c;
   return MSG_OK;

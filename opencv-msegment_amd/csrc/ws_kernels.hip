@@ -141,19 +141,41 @@ __global__ __launch_bounds__(BS) void k_prep(Ws ws, const int32_t* mk_in) {
 // `partial` (LDS, may be null) replaces the counts of the last chunk.  1024 threads.
 __device__ void column_scan(const int* cnt, int* coff, int nch, const int* partial, int* tail) {
   __shared__ int gs[4][NQ];
+  constexpr int MAXR = 32;  // per-thread chunk values kept in registers (nch <= 128)
   const int tid = threadIdx.x;
   const int lv = tid & (NQ - 1), g = tid >> 8;
   const int per = (nch + 3) >> 2;
   const int a = min(nch, g * per), b = min(nch, a + per);
-  int sum = 0;
-  for (int c = a; c < b; ++c) sum += (partial && c == nch - 1) ? partial[lv] : cnt[(long long)c * NQ + lv];
-  gs[g][lv] = sum;
-  __syncthreads();
-  int base = tail[lv];
-  for (int k = 0; k < g; ++k) base += gs[k][lv];
-  for (int c = a; c < b; ++c) {
-    coff[(long long)c * NQ + lv] = base;
-    base += (partial && c == nch - 1) ? partial[lv] : cnt[(long long)c * NQ + lv];
+  if (per <= MAXR) {
+    int v[MAXR];
+#pragma unroll
+    for (int k = 0; k < MAXR; ++k) {  // all loads issued back to back
+      const int c = a + k;
+      v[k] = (c < b) ? ((partial && c == nch - 1) ? partial[lv] : cnt[(long long)c * NQ + lv]) : 0;
+    }
+    int sum = 0;
+#pragma unroll
+    for (int k = 0; k < MAXR; ++k) sum += v[k];
+    gs[g][lv] = sum;
+    __syncthreads();
+    int base = tail[lv];
+    for (int k = 0; k < g; ++k) base += gs[k][lv];
+#pragma unroll
+    for (int k = 0; k < MAXR; ++k) {
+      if (a + k < b) coff[(long long)(a + k) * NQ + lv] = base;
+      base += v[k];
+    }
+  } else {
+    int sum = 0;
+    for (int c = a; c < b; ++c) sum += (partial && c == nch - 1) ? partial[lv] : cnt[(long long)c * NQ + lv];
+    gs[g][lv] = sum;
+    __syncthreads();
+    int base = tail[lv];
+    for (int k = 0; k < g; ++k) base += gs[k][lv];
+    for (int c = a; c < b; ++c) {
+      coff[(long long)c * NQ + lv] = base;
+      base += (partial && c == nch - 1) ? partial[lv] : cnt[(long long)c * NQ + lv];
+    }
   }
   __syncthreads();
   if (g == 0) tail[lv] += gs[0][lv] + gs[1][lv] + gs[2][lv] + gs[3][lv];
@@ -426,10 +448,18 @@ __device__ __forceinline__ void gather_label(const Ws& ws, const Seg* segs, int 
   }
 }
 
-__global__ __launch_bounds__(BS) void k_resolve(Ws ws) {
+__device__ __forceinline__ void small_loop(const Ws& ws);
+
+// Small batches (<= SMALL_MAX) are handed to block 0's single-workgroup loop (small_loop), which
+// processes the following small batches too; every other block returns.
+__global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
   if (B.n == 0 || B.mode != 0 || ctl->error) return;
+  if (B.n <= SMALL_MAX) {
+    if (blockIdx.x == 0) small_loop(ws);
+    return;
+  }
   __shared__ Seg segs[NQ];
   load_segs(ctl, B, segs);
   __syncthreads();
@@ -437,7 +467,7 @@ __global__ __launch_bounds__(BS) void k_resolve(Ws ws) {
   const unsigned long long etag = (unsigned long long)B.epoch << 32;
   const long long W = ws.W;
   unsigned long long* const dg = ws.diag;
-  for (int base = blockIdx.x * BS; base < B.n; base += gridDim.x * BS) {
+  for (int base = blockIdx.x * RBS; base < B.n; base += gridDim.x * RBS) {
     const int wbase = base + (tid & ~63);
     const int i = wbase + lane;
     const bool valid = i < B.n;
@@ -543,7 +573,7 @@ __global__ __launch_bounds__(BS) void k_resolve(Ws ws) {
 __global__ __launch_bounds__(BS) void k_claim(Ws ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
-  if (B.n == 0 || B.mode != 0 || ctl->error) return;
+  if (B.n == 0 || B.mode != 0 || ctl->error || ctl->skip) return;
   __shared__ int hist[NQ];
   __shared__ Seg segs[NQ];
   __shared__ int s_minpush;
@@ -604,6 +634,15 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
   const int tid = threadIdx.x;
+  if (ctl->skip) {  // k_resolve ran small batches and left an unresolved large one: next iteration
+    __syncthreads();
+    if (tid == 0) {
+      ctl->skip = 0;
+      ctl->cbat.n = 0;
+      ctl->cbat.nchunk = 0;
+    }
+    return;
+  }
   if (B.n == 0 || ctl->error) {  // nothing committed this iteration (finished, or stopped)
     __syncthreads();
     if (tid == 0) {
@@ -681,6 +720,8 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
     if (ns > 0) ctl->batches += 1;
     else ctl->done = 1;
   }
+  const int q = block_sum(tid < NQ ? ctl->qtail[tid] - ctl->qhead[tid] : 0);
+  if (tid == 0) ctl->remaining = q;
 }
 
 // Stable rank of this lane's pushes among the wave's pushes of the same level, in (lane, dir)
@@ -897,7 +938,7 @@ __device__ __forceinline__ bool attempt_item(const Item& it, F fetch, int& lab_o
   return true;
 }
 
-__global__ __launch_bounds__(1024) void k_small(Ws ws) {
+__device__ __forceinline__ void small_loop(const Ws& ws) {
   constexpr int NW = 16;
   Ctl* ctl = ws.ctl;
   __shared__ int s_lab[SMALL_MAX];
@@ -1095,6 +1136,8 @@ __global__ __launch_bounds__(1024) void k_small(Ws ws) {
     ctl->qhead[tid] = s_head[tid];
     ctl->qtail[tid] = s_tail[tid];
   }
+  const int q = block_sum(tid < NQ ? s_tail[tid] - s_head[tid] : 0);
+  if (tid == 0) ctl->remaining = q;
   for (int k = tid; k < s_B.nseg; k += 1024) ctl->seg[k] = s_seg[k];
   if (tid == 0) {
     ctl->bat = s_B;
@@ -1107,6 +1150,9 @@ __global__ __launch_bounds__(1024) void k_small(Ws ws) {
     ctl->pushes += nb_push;
     if (s_err) ctl->error |= s_err;
     if (s_B.n == 0 && !s_err) ctl->done = 1;
+    // the next batch is large and has not been resolved in this launch: the rest of this
+    // iteration (k_claim, k_scan, k_scatter) must not touch it
+    if (s_B.n > 0) ctl->skip = 1;
   }
 }
 

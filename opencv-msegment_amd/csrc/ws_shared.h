@@ -16,7 +16,7 @@ constexpr int INQ = -2;          // cv::watershed IN_QUEUE, before the pixel has
 __host__ __device__ inline int queued_state(int slot) { return -3 - slot; }
 __host__ __device__ inline int state_slot(int state) { return -3 - state; }
 constexpr int NONE = 0x7fffffff;
-constexpr int RES_GRID_MAX = 1024; // <= 4 blocks of 256 threads per CU: all co-resident
+constexpr int RBS = 1024;          // threads per k_resolve block (also the small-batch workgroup)
 constexpr int SMALL_MAX = 4096;    // batches up to this size run inside the one-workgroup k_small
 constexpr int PAL_LDS_MAX = 16384; // palettes up to this many labels are staged in LDS
 constexpr int MERGE_CAP = 1 << 22; // largest multi-segment batch (items)
@@ -63,8 +63,10 @@ struct Ctl {
   int cut;      // first rank of the current batch that pushes below its own level (NONE: none)
   int segcut;   // first segment invalidated by a push below its level (NONE: none)
   int minpush;  // lowest level pushed by the current batch (merge heuristic)
+  int skip;     // k_resolve ran small batches and left a large one unresolved: skip this iteration
   int done;
   int error;
+  int remaining;  // queued items after the last batch was formed (host polling hint)
   long long batches;
   long long pops;
   long long items;   // sum of batch sizes resolved (committed or not)
