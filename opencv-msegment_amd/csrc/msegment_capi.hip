@@ -228,7 +228,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   const int npx = (int)((N + CH - 1) / CH);
   const int gres = std::max(1, std::min(c->res_grid, (int)((N + RBS - 1) / RBS)));
   const int gclaim = std::min(npx * (CH / BS), 1024);
-  const int gsc = std::min(npx, 1024);
+  const int gsc = std::min(npx * (CH / 1024), 1024);
   HIPCHK(c, hipMemsetAsync(c->d_ctl, 0, sizeof(Ctl), st));
   if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 8 * sizeof(unsigned long long), st));
   HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)npx * NQ * sizeof(int32_t), st));

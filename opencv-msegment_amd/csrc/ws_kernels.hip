@@ -695,9 +695,7 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
     cb.nchunk = nch;
     ctl->cbat = cb;
   }
-  // every histogram row this batch accumulated into is consumed: zero it for the next batch
-  const long long rows = (long long)((B.n + CH - 1) / CH) * NQ;
-  for (long long k = tid; k < rows; k += blockDim.x) ws.cnt[k] = 0;
+  // the histogram rows this batch accumulated are zeroed by k_scatter (cbat.n covers them all)
   __syncthreads();
   form_batch(ctl->qbase, ctl->qhead, ctl->qtail, B.mode == 0 ? ctl->minpush : 0, nsegs, &s_nseg, &s_n);
   __syncthreads();
@@ -759,77 +757,84 @@ __device__ __forceinline__ void wave_rank(unsigned mask, unsigned lvls, int pos[
 
 // Ordered scatter: commit labels of the committed prefix and append its pushes to the buckets in
 // exact (rank, dir) order.  mode 1 (phase-1 pseudo-batch): item i is pixel ilist[i] itself.
-// 1024 threads = 16 waves: a 4096-item chunk is 4 sub-rounds.
+// One 1024-thread block per 1024-item sub-round, four per 4096-item chunk, all independent: a
+// sub-round's in-chunk offset is the chunk offset (k_scan) plus the per-level push counts of the
+// chunk's earlier sub-rounds, recounted here from their (L2-resident) descriptors.  The blocks
+// also zero the histogram rows the batch accumulated (consumed by k_scan).
 __global__ __launch_bounds__(1024) void k_scatter(Ws ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->cbat;
   if (B.nchunk == 0 || ctl->error) return;
-  constexpr int NW = 16;
+  constexpr int NW = 16, SUBS = CH / 1024;
   __shared__ int run[NQ];
-  __shared__ int tot[NQ];
   __shared__ int wcnt[NW][NQ];
   __shared__ int qb[NQ];
   const int tid = threadIdx.x, wv = tid >> 6;
   const long long W = ws.W;
+  {
+    const long long rows = (long long)((B.n + CH - 1) / CH) * NQ;
+    for (long long k = (long long)blockIdx.x * 1024 + tid; k < rows; k += (long long)gridDim.x * 1024)
+      ws.cnt[k] = 0;
+  }
   if (tid < NQ) qb[tid] = ctl->qbase[tid];
-  for (int ch = blockIdx.x; ch < B.nchunk; ch += gridDim.x) {
+  for (int vb = blockIdx.x; vb < B.nchunk * SUBS; vb += gridDim.x) {
+    const int ch = vb / SUBS, i0 = ch * CH + (vb % SUBS) * 1024;
+    if (i0 >= B.ncommit) continue;  // block-uniform
     if (tid < NQ) {
       run[tid] = ws.coff[(long long)ch * NQ + tid];
 #pragma unroll
       for (int k = 0; k < NW; ++k) wcnt[k][tid] = 0;
     }
     __syncthreads();
-    for (int i0 = ch * CH; i0 < min(ch * CH + CH, B.ncommit); i0 += 1024) {  // block-uniform
-      const int i = i0 + tid;
-      const bool valid = i < B.ncommit;
-      unsigned mask = 0, lvls = 0;
-      long long p = 0;
-      if (valid) {
-        const unsigned long long d = ws.desc[i];
-        mask = (unsigned)(d >> 32) & 15u;
-        lvls = (unsigned)d;
-        if (B.mode == 0) {
-          p = ws.ipx[i];
-          ws.mk[p] = (int32_t)(uint32_t)ws.tl[i];
-        } else {
-          p = ws.ilist[i];
-        }
-      }
-      int pos[4] = {0, 0, 0, 0};
-      wave_rank(mask, lvls, pos, wcnt[wv]);
-      __syncthreads();
-      if (tid < NQ) {  // exclusive prefix over the waves, per level
-        int acc = 0;
+    for (int j = ch * CH + tid; j < i0; j += 1024) {  // earlier sub-rounds of this chunk
+      const unsigned long long d = ws.desc[j];
+      const unsigned m = (unsigned)(d >> 32) & 15u;
 #pragma unroll
-        for (int k = 0; k < NW; ++k) {
-          const int t = wcnt[k][tid];
-          wcnt[k][tid] = acc;
-          acc += t;
-        }
-        tot[tid] = acc;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        if (!((mask >> d) & 1u)) continue;
-        const int lv = (lvls >> (8 * d)) & 255;
-        const int dest = qb[lv] + run[lv] + wcnt[wv][lv] + pos[d];
-        if (dest < 0 || (long long)dest >= ws.qcap) {
-          atomicOr(&ctl->error, ERR_CAPACITY);
-          continue;
-        }
-        const long long n = (B.mode == 0) ? nb_of(p, d, W) : p;
-        ws.mk[n] = queued_state(dest);
-        ws.qbuf[dest] = (int32_t)n;
-      }
-      __syncthreads();
-      if (tid < NQ) {
-        run[tid] += tot[tid];
-#pragma unroll
-        for (int k = 0; k < NW; ++k) wcnt[k][tid] = 0;
-      }
-      __syncthreads();
+      for (int k = 0; k < 4; ++k)
+        if ((m >> k) & 1u) atomicAdd(&run[(d >> (8 * k)) & 255], 1);
     }
+    const int i = i0 + tid;
+    const bool valid = i < B.ncommit;
+    unsigned mask = 0, lvls = 0;
+    long long p = 0;
+    if (valid) {
+      const unsigned long long d = ws.desc[i];
+      mask = (unsigned)(d >> 32) & 15u;
+      lvls = (unsigned)d;
+      if (B.mode == 0) {
+        p = ws.ipx[i];
+        ws.mk[p] = (int32_t)(uint32_t)ws.tl[i];
+      } else {
+        p = ws.ilist[i];
+      }
+    }
+    int pos[4] = {0, 0, 0, 0};
+    wave_rank(mask, lvls, pos, wcnt[wv]);
+    __syncthreads();
+    if (tid < NQ) {  // exclusive prefix over the waves, per level, on top of the sub-round offset
+      int acc = run[tid];
+#pragma unroll
+      for (int k = 0; k < NW; ++k) {
+        const int t = wcnt[k][tid];
+        wcnt[k][tid] = acc;
+        acc += t;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      if (!((mask >> d) & 1u)) continue;
+      const int lv = (lvls >> (8 * d)) & 255;
+      const int dest = qb[lv] + wcnt[wv][lv] + pos[d];
+      if (dest < 0 || (long long)dest >= ws.qcap) {
+        atomicOr(&ctl->error, ERR_CAPACITY);
+        continue;
+      }
+      const long long n = (B.mode == 0) ? nb_of(p, d, W) : p;
+      ws.mk[n] = queued_state(dest);
+      ws.qbuf[dest] = (int32_t)n;
+    }
+    __syncthreads();  // before the next sub-round reuses run/wcnt
   }
 }
 
