@@ -227,7 +227,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
 
   const int npx = (int)((N + CH - 1) / CH);
   const int gres = std::max(1, std::min(c->res_grid, (int)((N + RBS - 1) / RBS)));
-  const int gclaim = std::min(npx * (CH / BS), 1024);
+  const int gclaim = std::min(npx * (CH / 1024), 256);
   const int gsc = std::min(npx * (CH / 1024), 1024);
   HIPCHK(c, hipMemsetAsync(c->d_ctl, 0, sizeof(Ctl), st));
   if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 8 * sizeof(unsigned long long), st));
@@ -245,8 +245,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   for (;;) {
     for (int g = 0; g < c->group; ++g, ++it) {
       LAUNCH(c, KID_RESOLVE, st, k_resolve, dim3(gres), dim3(RBS), 0, ws);
-      LAUNCH(c, KID_CLAIM, st, k_claim, dim3(gclaim), dim3(BS), 0, ws);
-      LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
+      LAUNCH(c, KID_CLAIM, st, k_claim, dim3(gclaim), dim3(1024), 0, ws);  // + scan (last block)
       LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws);
     }
     HIPCHK(c, hipGetLastError());

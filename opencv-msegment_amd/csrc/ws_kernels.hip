@@ -182,13 +182,15 @@ __device__ void column_scan(const int* cnt, int* coff, int nch, const int* parti
   __syncthreads();
 }
 
-__device__ int block_sum(int v) {
-  __shared__ int acc;
-  if (threadIdx.x == 0) acc = 0;
+__device__ int block_sum(int v) {  // every thread of the block calls; result to all
+  __shared__ int part[32];
+  const int nw = (blockDim.x + 63) >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (lane_id() == 0) part[threadIdx.x >> 6] = v;
   __syncthreads();
-  if (v) atomicAdd(&acc, v);
-  __syncthreads();
-  const int r = acc;
+  int r = 0;
+  for (int k = 0; k < nw; ++k) r += part[k];
   __syncthreads();
   return r;
 }
@@ -570,19 +572,25 @@ __global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
 // after the item) and the segment cut (push below a LATER segment's level: end the batch before
 // that segment), and the lowest pushed level.  No waiting: every claim of the batch was made
 // before this kernel started.
-__global__ __launch_bounds__(BS) void k_claim(Ws ws) {
+__device__ void scan_body(const Ws& ws);
+
+// Claim check + per-chunk level histograms, 1024-thread blocks.  The last block to finish (atomic
+// ticket, agent-scope fences on both sides) runs the scan itself, saving a kernel boundary per
+// iteration; when there is nothing to claim (small-loop skip, phase-1 pseudo-batch, end, error)
+// block 0 runs it alone.
+__global__ __launch_bounds__(1024) void k_claim(Ws ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
-  if (B.n == 0 || B.mode != 0 || ctl->error || ctl->skip) return;
+  const bool work = !(B.n == 0 || B.mode != 0 || ctl->error || ctl->skip);
   __shared__ int hist[NQ];
   __shared__ Seg segs[NQ];
   __shared__ int s_minpush;
-  load_segs(ctl, B, segs);
+  if (work) load_segs(ctl, B, segs);
   if (threadIdx.x == 0) s_minpush = NQ;
   const int tid = threadIdx.x;
   const long long W = ws.W;
-  for (int base = blockIdx.x * BS; base < B.n; base += gridDim.x * BS) {
-    hist[tid] = 0;
+  for (int base = blockIdx.x * 1024; work && base < B.n; base += gridDim.x * 1024) {
+    if (tid < NQ) hist[tid] = 0;
     __syncthreads();
     const int i = base + tid;
     if (i < B.n) {
@@ -620,17 +628,35 @@ __global__ __launch_bounds__(BS) void k_claim(Ws ws) {
       }
     }
     __syncthreads();
-    if (hist[tid]) atomicAdd(&ws.cnt[(long long)(base / CH) * NQ + tid], hist[tid]);
+    if (tid < NQ && hist[tid]) atomicAdd(&ws.cnt[(long long)(base / CH) * NQ + tid], hist[tid]);
     __syncthreads();
   }
   if (tid == 0 && s_minpush < NQ) atomicMin(&ctl->minpush, s_minpush);
+  // arrival ticket (every path takes it: no block may read ctl->bat after the scan rewrote it).
+  // Publish: drain every wave, barrier, ONE agent release fence, drain, relaxed ticket add.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(&ctl->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hist[0] = (t == gridDim.x - 1);
+    if (t == gridDim.x - 1) {  // last arriver: acquire before reading the other blocks' output
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ctl->ticket = 0;
+    }
+  }
+  __syncthreads();
+  if (!hist[0]) return;
+  scan_body(ws);
 }
 
 // ---------------------------------------------------------------------------------------------
 // Scan (1 block x 1024): committed prefix (interrupt cut, segment cut), recount of the cut chunk,
 // column scan -> per-chunk bucket offsets, head/tail update, hand the committed batch to k_scatter
 // (cbat), form the next batch.
-__global__ __launch_bounds__(1024) void k_scan(Ws ws) {
+__device__ void scan_body(const Ws& ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
   const int tid = threadIdx.x;
@@ -655,20 +681,29 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
     }
     return;
   }
+  // the queue state lives in LDS for the whole kernel: one parallel load, one write-back
   __shared__ int partial[NQ];
+  __shared__ int s_head[NQ], s_tail[NQ], s_base[NQ];
+  __shared__ Seg s_seg[NQ];
   __shared__ Seg nsegs[NQ];
   __shared__ int s_nseg, s_n;
+  if (tid < NQ) {
+    s_head[tid] = ctl->qhead[tid];
+    s_tail[tid] = ctl->qtail[tid];
+    s_base[tid] = ctl->qbase[tid];
+    partial[tid] = 0;
+  }
+  if (B.mode == 0 && tid < B.nseg) s_seg[tid] = ctl->seg[tid];
+  const int cut = ctl->cut, segcut = ctl->segcut, minpush = ctl->minpush;
+  __syncthreads();
   int ncommit = B.n;
   if (B.mode == 0) {
-    const int cut = ctl->cut, segcut = ctl->segcut;
     if (cut != NONE) ncommit = min(ncommit, cut + 1);
-    if (segcut != NONE) ncommit = min(ncommit, ctl->seg[segcut].rank);
+    if (segcut != NONE) ncommit = min(ncommit, s_seg[segcut].rank);
   }
   const int nch = (ncommit + CH - 1) / CH;
   const bool haspartial = (ncommit % CH) != 0 && ncommit != B.n;
-  if (haspartial) {
-    if (tid < NQ) partial[tid] = 0;
-    __syncthreads();
+  if (haspartial) {  // the cut chunk's histogram covers items past the cut: recount its prefix
     for (int i = (nch - 1) * CH + tid; i < ncommit; i += blockDim.x) {
       const unsigned long long d = ws.desc[i];
       const unsigned m = (unsigned)(d >> 32) & 15u;
@@ -677,12 +712,12 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
     }
     __syncthreads();
   }
-  const int oldt = (tid < NQ) ? ctl->qtail[tid] : 0;
-  column_scan(ws.cnt, ws.coff, nch, haspartial ? partial : nullptr, ctl->qtail);
-  const int npush = block_sum((tid < NQ) ? ctl->qtail[tid] - oldt : 0);
+  const int oldt = (tid < NQ) ? s_tail[tid] : 0;
+  column_scan(ws.cnt, ws.coff, nch, haspartial ? partial : nullptr, s_tail);
+  const int npush = block_sum((tid < NQ) ? s_tail[tid] - oldt : 0);
   if (B.mode == 0 && tid < B.nseg) {  // advance every segment's bucket head by what it committed
-    const Seg s = ctl->seg[tid];
-    ctl->qhead[s.L] += max(0, min(ncommit - s.rank, s.n));
+    const Seg s = s_seg[tid];
+    s_head[s.L] += max(0, min(ncommit - s.rank, s.n));
   }
   if (tid == 0) {
     ctl->pushes += npush;
@@ -697,10 +732,14 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
   }
   // the histogram rows this batch accumulated are zeroed by k_scatter (cbat.n covers them all)
   __syncthreads();
-  form_batch(ctl->qbase, ctl->qhead, ctl->qtail, B.mode == 0 ? ctl->minpush : 0, nsegs, &s_nseg, &s_n);
+  form_batch(s_base, s_head, s_tail, B.mode == 0 ? minpush : 0, nsegs, &s_nseg, &s_n);
   __syncthreads();
   const int ns = s_nseg;
   for (int k = tid; k < ns; k += blockDim.x) ctl->seg[k] = nsegs[k];
+  if (tid < NQ) {
+    ctl->qhead[tid] = s_head[tid];
+    ctl->qtail[tid] = s_tail[tid];
+  }
   if (tid == 0) {
     Batch nb;
     nb.mode = 0;
@@ -718,9 +757,11 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
     if (ns > 0) ctl->batches += 1;
     else ctl->done = 1;
   }
-  const int q = block_sum(tid < NQ ? ctl->qtail[tid] - ctl->qhead[tid] : 0);
+  const int q = block_sum(tid < NQ ? s_tail[tid] - s_head[tid] : 0);
   if (tid == 0) ctl->remaining = q;
 }
+
+__global__ __launch_bounds__(1024) void k_scan(Ws ws) { scan_body(ws); }
 
 // Stable rank of this lane's pushes among the wave's pushes of the same level, in (lane, dir)
 // order.  Writes the per-level wave totals to wrow[level].  Wave-uniform loop over the distinct

@@ -64,6 +64,7 @@ struct Ctl {
   int segcut;   // first segment invalidated by a push below its level (NONE: none)
   int minpush;  // lowest level pushed by the current batch (merge heuristic)
   int skip;     // k_resolve ran small batches and left a large one unresolved: skip this iteration
+  unsigned ticket;  // k_claim blocks finished this iteration (the last one runs the scan)
   int done;
   int error;
   int remaining;  // queued items after the last batch was formed (host polling hint)
