@@ -29,7 +29,7 @@ METRIC = "Mpixels/sec segmented at 4096x4096 RGB; achieved HBM GB/s vs peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
 # Algorithmic bytes (DESIGN.md "Kernels"): what each kernel must move at minimum per unit.
-BYTES_PER_PIXEL = {"k_prep": 13.0, "k_colorize": 7.0, "k_edge_weights": 5.0}
+BYTES_PER_PIXEL = {"k_prep": 15.0, "k_untile": 15.0, "k_colorize": 7.0, "k_edge_weights": 5.0}
 BYTES_PER_ITEM = {"k_resolve": 40.0}        # per batch item resolved
 BYTES_SCATTER = (24.0, 12.0)                # per committed item, per appended push
 E2E_BYTES_PER_PIXEL = 14.0                  # 3 B BGR + 4 B markers in, 4 B labels + 3 B BGR out

@@ -27,10 +27,9 @@ struct msg_ctx {
   hipStream_t own = nullptr;
   std::string err;
   Ctl* d_ctl = nullptr;
-  // flood workspace (sized for cap_n pixels)
-  long long cap_n = 0;
-  uint32_t* d_w4 = nullptr;
-  uint8_t* d_lv1 = nullptr;
+  // flood workspace (sized for cap_n pixels, cap_np tiled pixel words, cap_rc raster chunks)
+  long long cap_n = 0, cap_np = 0, cap_rc = 0;
+  int32_t* d_px = nullptr;  // tiled {state, w4} words
   int32_t *d_qbuf = nullptr, *d_ilist = nullptr;
   int32_t *d_cnt = nullptr, *d_coff = nullptr, *d_tot = nullptr, *d_choff = nullptr;
   unsigned long long *d_tl = nullptr, *d_desc = nullptr, *d_claim = nullptr;
@@ -64,10 +63,10 @@ struct msg_ctx {
 namespace {
 
 enum KernelId { KID_PREP, KID_INIT_SCAN, KID_COMPACT, KID_RESOLVE, KID_SCAN, KID_SCATTER,
-                KID_COLORIZE, KID_EDGE, KID_SMALL, KID_CLAIM };
+                KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_CLAIM };
 const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_compact", "k_resolve",
                                                 "k_scan", "k_scatter", "k_colorize",
-                                                "k_edge_weights", "k_small", "k_claim"};
+                                                "k_edge_weights", "k_untile", "k_claim"};
 
 hipEvent_t pool_event(msg_ctx* c) {
   if (c->evused == c->evpool.size()) {
@@ -133,11 +132,11 @@ void dfree(T*& p) {
 }
 
 void free_flood(msg_ctx* c) {
-  dfree(c->d_w4); dfree(c->d_lv1);
+  dfree(c->d_px);
   dfree(c->d_qbuf); dfree(c->d_ilist);
   dfree(c->d_cnt); dfree(c->d_coff); dfree(c->d_tot); dfree(c->d_choff);
   dfree(c->d_tl); dfree(c->d_desc); dfree(c->d_claim);
-  c->cap_n = 0;
+  c->cap_n = c->cap_np = c->cap_rc = 0;
   c->qcap = 0;
 }
 
@@ -146,26 +145,31 @@ void free_stage(msg_ctx* c) {
   c->stage_n = 0;
 }
 
-int ensure_flood(msg_ctx* c, long long N) {
-  if (N <= c->cap_n) return MSG_OK;
+int ensure_flood(msg_ctx* c, int H, int W) {
+  const long long N = (long long)H * W;
+  const long long Np = (long long)((H + 3) / 4) * ((W + 3) / 4) * 16;
+  const long long nrc = (long long)H * ((W + RSEG - 1) / RSEG);
+  if (N <= c->cap_n && Np <= c->cap_np && nrc <= c->cap_rc) return MSG_OK;
+  const long long n = std::max(N, c->cap_n), np = std::max(Np, c->cap_np), rc = std::max(nrc, c->cap_rc);
   free_flood(c);
-  const long long nch = (N + CH - 1) / CH;
-  const long long qcap = 4 * N + 16;
-  HIPCHK(c, hipMalloc((void**)&c->d_w4, N * 4));
-  HIPCHK(c, hipMalloc((void**)&c->d_lv1, N));
-  HIPCHK(c, hipMalloc((void**)&c->d_ilist, N * 4));
+  const long long nch = (n + CH - 1) / CH;
+  const long long qcap = 4 * n + 16;
+  HIPCHK(c, hipMalloc((void**)&c->d_px, np * 8));
+  HIPCHK(c, hipMalloc((void**)&c->d_ilist, n * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_qbuf, qcap * 4));
-  HIPCHK(c, hipMalloc((void**)&c->d_tl, N * 8));
-  HIPCHK(c, hipMalloc((void**)&c->d_desc, N * 8));
+  HIPCHK(c, hipMalloc((void**)&c->d_tl, n * 8));
+  HIPCHK(c, hipMalloc((void**)&c->d_desc, n * 8));
   HIPCHK(c, hipMalloc((void**)&c->d_cnt, nch * NQ * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_coff, nch * NQ * 4));
-  HIPCHK(c, hipMalloc((void**)&c->d_tot, nch * 4));
-  HIPCHK(c, hipMalloc((void**)&c->d_choff, nch * 4));
-  HIPCHK(c, hipMalloc((void**)&c->d_claim, N * 8));
-  HIPCHK(c, hipMemset(c->d_tl, 0, N * 8));
-  HIPCHK(c, hipMemset(c->d_claim, 0, N * 8));
+  HIPCHK(c, hipMalloc((void**)&c->d_tot, rc * 4));
+  HIPCHK(c, hipMalloc((void**)&c->d_choff, rc * 4));
+  HIPCHK(c, hipMalloc((void**)&c->d_claim, np * 8));
+  HIPCHK(c, hipMemset(c->d_tl, 0, n * 8));
+  HIPCHK(c, hipMemset(c->d_claim, 0, np * 8));
   c->epoch = 1;
-  c->cap_n = N;
+  c->cap_n = n;
+  c->cap_np = np;
+  c->cap_rc = rc;
   c->qcap = qcap;
   return MSG_OK;
 }
@@ -183,31 +187,31 @@ int ensure_stage(msg_ctx* c, long long N) {
 
 int check_size(msg_ctx* c, int rows, int cols) {
   if (rows < 0 || cols < 0) return fail(c, MSG_EINVAL, "negative size %d x %d", rows, cols);
-  if ((long long)rows * cols > (1ll << 29))
+  if ((long long)rows * cols > (1ll << 28))
     return fail(c, MSG_EINVAL, "frame too large for one context: %d x %d", rows, cols);
   return MSG_OK;
 }
 
-// The exact flood on device buffers.  d_mk_in may alias d_mk.
-int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t* d_mk, int H,
-              int W, hipStream_t st) {
+// The exact flood on device buffers, in the context's tiled workspace, then the row-major label
+// map into d_labels (may alias d_mk_in) fused with the colourisation when d_dst is given.
+int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t* d_labels, int H,
+              int W, hipStream_t st, int depth = 0, const uint8_t* d_pal = nullptr,
+              uint8_t* d_dst = nullptr, uint8_t* d_gray = nullptr) {
   const long long N = (long long)H * W;
   c->stats = msg_stats{};
   c->stats.rows = H;
   c->stats.cols = W;
   if (N == 0) return MSG_OK;
-  int rc = ensure_flood(c, N);
+  int rc = ensure_flood(c, H, W);
   if (rc) return rc;
-  if (c->epoch > 0xF0000000u) {
+  if (c->epoch > 0x70000000u) {  // granule bit 63 flags a provisional value
     HIPCHK(c, hipMemsetAsync(c->d_tl, 0, c->cap_n * 8, st));
-    HIPCHK(c, hipMemsetAsync(c->d_claim, 0, c->cap_n * 8, st));
+    HIPCHK(c, hipMemsetAsync(c->d_claim, 0, c->cap_np * 8, st));
     c->epoch = 1;
   }
   Ws ws;
   ws.img = d_img;
-  ws.mk = d_mk;
-  ws.w4 = c->d_w4;
-  ws.lv1 = c->d_lv1;
+  ws.mk = c->d_px;
   ws.qbuf = c->d_qbuf;
   ws.ilist = c->d_ilist;
   ws.tl = c->d_tl;
@@ -222,6 +226,8 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   ws.diag = c->diag ? c->d_diag : nullptr;
   ws.H = H;
   ws.W = W;
+  ws.Wt = (W + 3) / 4;
+  ws.nseg = (W + RSEG - 1) / RSEG;
   ws.N = N;
   ws.qcap = c->qcap;
 
@@ -232,9 +238,10 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   HIPCHK(c, hipMemsetAsync(c->d_ctl, 0, sizeof(Ctl), st));
   if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 8 * sizeof(unsigned long long), st));
   HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)npx * NQ * sizeof(int32_t), st));
-  LAUNCH(c, KID_PREP, st, k_prep, dim3(npx), dim3(BS), 0, ws, d_mk_in);
-  LAUNCH(c, KID_INIT_SCAN, st, k_init_scan, dim3(1), dim3(1024), 0, ws, npx, c->epoch);
-  LAUNCH(c, KID_COMPACT, st, k_compact, dim3(npx), dim3(BS), 0, ws);
+  const int nrc = H * ws.nseg;  // raster chunks
+  LAUNCH(c, KID_PREP, st, k_prep, dim3((H + 3) / 4 * ws.nseg), dim3(256), 0, ws, d_mk_in);
+  LAUNCH(c, KID_INIT_SCAN, st, k_init_scan, dim3(1), dim3(1024), 0, ws, nrc, c->epoch);
+  LAUNCH(c, KID_COMPACT, st, k_compact, dim3(nrc), dim3(256), 0, ws);
   LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
   LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws);
   HIPCHK(c, hipGetLastError());
@@ -266,6 +273,14 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
     }
     prev = slot;
     slot ^= 1;
+  }
+  {
+    const long long ntiles = (long long)((H + 3) / 4) * ws.Wt;
+    const int grid = (int)std::min<long long>((ntiles + 255) / 256, 4096);
+    const size_t shm = (d_dst && d_pal && depth <= PAL_LDS_MAX) ? (size_t)std::max(depth, 1) * 4 : 0;
+    LAUNCH(c, KID_UNTILE, st, k_untile, dim3(grid), dim3(256), shm, c->d_px, H, W, ws.Wt, d_labels,
+           depth, d_pal, d_dst, d_gray);
+    HIPCHK(c, hipGetLastError());
   }
   Ctl tail;
   HIPCHK(c, hipMemcpyAsync(&tail, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
@@ -344,9 +359,9 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
       msg_destroy(c);
       return MSG_EHIP;
     }
-    // one 1024-thread block per CU (k_resolve is VGPR-limited to 16 waves/CU); never trust a
-    // larger occupancy answer for a grid whose blocks wait on each other
-    c->res_grid = cus * std::min(per, 1);
+    // blocks of a k_resolve round wait on each other, so the grid must be co-resident: the
+    // occupancy answer (2 x 1024 threads per CU at k_resolve's 48 VGPRs), capped at 2
+    c->res_grid = cus * std::max(1, std::min(per, 2));
   }
   *out = c;
   return MSG_OK;
@@ -447,9 +462,17 @@ int msg_watershed_colorize_dev(msg_ctx* c, const void* d_bgr, const void* d_mark
                                void* d_labels, int rows, int cols, int depth,
                                const void* d_palette_bgr, void* d_dst_bgr, void* d_gray,
                                void* stream) {
-  int rc = msg_watershed_dev(c, d_bgr, d_markers_in, d_labels, rows, cols, stream);
+  if (!c) return MSG_EINVAL;
+  int rc = check_size(c, rows, cols);
   if (rc) return rc;
-  return msg_colorize_dev(c, d_labels, rows, cols, depth, d_palette_bgr, d_dst_bgr, d_gray, stream);
+  if (depth < 0) return fail(c, MSG_EINVAL, "negative depth");
+  if ((long long)rows * cols > 0 && (!d_bgr || !d_markers_in || !d_labels || !d_dst_bgr))
+    return fail(c, MSG_EINVAL, "null device pointer");
+  HIPCHK(c, hipSetDevice(c->dev));
+  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  return run_flood(c, (const uint8_t*)d_bgr, (const int32_t*)d_markers_in, (int32_t*)d_labels, rows,
+                   cols, st, depth, (const uint8_t*)d_palette_bgr, (uint8_t*)d_dst_bgr,
+                   (uint8_t*)d_gray);
 }
 
 int msg_edge_weights_dev(msg_ctx* c, const void* d_bgr, void* d_wright, void* d_wdown, int rows,
@@ -504,21 +527,18 @@ int msg_watershed_colorize(msg_ctx* c, const uint8_t* bgr, size_t bgr_stride, in
                              hipMemcpyHostToDevice, st));
   HIPCHK(c, hipMemcpy2DAsync(c->d_mk, (size_t)cols * 4, markers, marker_stride, (size_t)cols * 4,
                              rows, hipMemcpyHostToDevice, st));
-  rc = run_flood(c, c->d_img, c->d_mk, c->d_mk, rows, cols, st);
+  const uint8_t* dp = nullptr;
+  if (want_color && palette_bgr && depth > 0) {
+    rc = upload_palette(c, palette_bgr, depth, st);
+    if (rc) return rc;
+    dp = c->d_pal;  // (depth 0: every pixel is background either way)
+  }
+  rc = run_flood(c, c->d_img, c->d_mk, c->d_mk, rows, cols, st, depth, dp,
+                 want_color ? c->d_dst : nullptr, (want_color && gray) ? c->d_gray : nullptr);
   if (rc) return rc;
   HIPCHK(c, hipMemcpy2DAsync(markers, marker_stride, c->d_mk, (size_t)cols * 4, (size_t)cols * 4,
                              rows, hipMemcpyDeviceToHost, st));
   if (want_color) {
-    const uint8_t* dp = nullptr;
-    if (palette_bgr && depth > 0) {
-      rc = upload_palette(c, palette_bgr, depth, st);
-      if (rc) return rc;
-      dp = c->d_pal;
-    } else if (palette_bgr) {
-      dp = nullptr;  // depth 0: every pixel is background either way
-    }
-    rc = launch_colorize(c, c->d_mk, N, depth, dp, c->d_dst, gray ? c->d_gray : nullptr, st);
-    if (rc) return rc;
     HIPCHK(c, hipMemcpy2DAsync(dst_bgr, dst_stride, c->d_dst, (size_t)cols * 3, (size_t)cols * 3,
                                rows, hipMemcpyDeviceToHost, st));
     if (gray)

@@ -72,68 +72,110 @@ __global__ __launch_bounds__(256) void k_edge_weights(const uint8_t* __restrict_
 
 // ---------------------------------------------------------------------------------------------
 // Phase 0 + phase 1 of cv::watershed (border, sanitise, initial queue levels) fused with the
-// colour-distance stencil and the bucket-capacity histogram.  One block = one CH-pixel chunk.
-// mk_in may alias ws.mk: a pixel's "> 0" status never changes here and frame neighbours are
-// excluded by coordinates, so the in-place rewrite is race-free.
-__global__ __launch_bounds__(BS) void k_prep(Ws ws, const int32_t* mk_in) {
+// colour-distance stencil and the bucket-capacity histogram.  One thread = one 4x4 tile (its
+// 128-B line of {state, w4} words written with 16-B stores), one block = a 4-row x RSEG-column
+// strip, i.e. 4 raster chunks, whose phase-1 counts feed the raster-order compaction.
+__device__ __forceinline__ uint32_t ld_bgr(const uint8_t* img, int r, int c, int H, int W) {
+  if (r < 0 || r >= H || c < 0 || c >= W) return 0;
+  const uint8_t* q = img + ((long long)r * W + c) * 3;
+  return (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16);
+}
+
+__device__ __forceinline__ int cdiffp(uint32_t a, uint32_t b) {  // L-inf BGR distance, packed
+  const int d0 = abs((int)(a & 255u) - (int)(b & 255u));
+  const int d1 = abs((int)((a >> 8) & 255u) - (int)((b >> 8) & 255u));
+  const int d2 = abs((int)((a >> 16) & 255u) - (int)((b >> 16) & 255u));
+  return max(max(d0, d1), d2);
+}
+
+__global__ __launch_bounds__(256) void k_prep(Ws ws, const int32_t* __restrict__ mk_in) {
+  static_assert(NQ == 256 && RSEG == 1024, "one thread per level and per tile of the strip");
   __shared__ unsigned caph[NQ];
-  __shared__ int ntot;
+  __shared__ int rowcnt[4];
   const int tid = threadIdx.x;
   caph[tid] = 0;
-  if (tid == 0) ntot = 0;
+  if (tid < 4) rowcnt[tid] = 0;
   __syncthreads();
-  const int H = ws.H, W = ws.W;
-  const long long N = ws.N;
-  const long long c0 = (long long)blockIdx.x * CH;
-  int mycount = 0;
-  for (int s = 0; s < SUB; ++s) {
-    const long long p = c0 + s * BS + tid;
-    if (p >= N) break;
-    const int r = (int)(p / W), c = (int)(p - (long long)r * W);
-    const uint8_t* ip = ws.img + p * 3;
-    const int wright = (c + 1 < W) ? cdiff3(ip, ip + 3) : 0;
-    const int wdown = (r + 1 < H) ? cdiff3(ip, ip + 3 * (long long)W) : 0;
-    const int wl = (c >= 1) ? cdiff3(ip, ip - 3) : 0;
-    const int wu = (r >= 1) ? cdiff3(ip, ip - 3 * (long long)W) : 0;
-    ws.w4[p] = (uint32_t)wl | ((uint32_t)wright << 8) | ((uint32_t)wu << 16) | ((uint32_t)wdown << 24);
-    int32_t out;
-    if (r == 0 || r == H - 1 || c == 0 || c == W - 1) {
-      out = WSHED;
-    } else {
-      const int32_t m = mk_in[p];
-      if (m > 0) {
-        out = m;
-      } else {
-        // interior neighbours (the frame is WSHED in the serial code and never counts)
-        const int wleft = (c >= 2) ? wl : -1;
-        const int wup = (r >= 2) ? wu : -1;
-        const int wr_i = (c <= W - 3) ? wright : -1;
-        const int wd_i = (r <= H - 3) ? wdown : -1;
-        int lvl = 256;
-        if (wleft >= 0 && mk_in[p - 1] > 0) lvl = min(lvl, wleft);
-        if (wr_i >= 0 && mk_in[p + 1] > 0) lvl = min(lvl, wr_i);
-        if (wup >= 0 && mk_in[p - W] > 0) lvl = min(lvl, wup);
-        if (wd_i >= 0 && mk_in[p + W] > 0) lvl = min(lvl, wd_i);
-        if (lvl < 256) {
-          out = INQ;
-          ws.lv1[p] = (uint8_t)lvl;
-          ++mycount;
-        } else {
-          out = 0;
-        }
-        // this pixel may be queued once, at one of its distinct interior edge weights
-        if (wleft >= 0) atomicAdd(&caph[wleft], 1u);
-        if (wr_i >= 0 && wr_i != wleft) atomicAdd(&caph[wr_i], 1u);
-        if (wup >= 0 && wup != wleft && wup != wr_i) atomicAdd(&caph[wup], 1u);
-        if (wd_i >= 0 && wd_i != wleft && wd_i != wr_i && wd_i != wup) atomicAdd(&caph[wd_i], 1u);
+  const int H = ws.H, W = ws.W, Wt = ws.Wt;
+  const int tr = blockIdx.x / ws.nseg, cs = blockIdx.x % ws.nseg;
+  const int tc = cs * (RSEG / 4) + tid;
+  int myrow[4] = {0, 0, 0, 0};
+  if (tc < Wt) {
+    const int r0 = tr * 4, c0 = tc * 4;
+    uint32_t px[6][6];  // colours of rows r0-1..r0+4, cols c0-1..c0+4 (0 outside the image)
+    unsigned pos[6];    // bit j: marker > 0 at (r0-1+i, c0-1+j)
+    int mv[4][4];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      pos[i] = 0;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int r = r0 - 1 + i, c = c0 - 1 + j;
+        px[i][j] = ld_bgr(ws.img, r, c, H, W);
+        const bool in = r >= 0 && r < H && c >= 0 && c < W;
+        const int m = in ? mk_in[(long long)r * W + c] : 0;
+        if (m > 0) pos[i] |= 1u << j;
+        if (i >= 1 && i <= 4 && j >= 1 && j <= 4) mv[i - 1][j - 1] = m;
       }
     }
-    ws.mk[p] = out;
+    int4* out = reinterpret_cast<int4*>(ws.mk + ((((long long)tr * Wt + tc) << 4) << 1));
+#pragma unroll
+    for (int ry = 0; ry < 4; ++ry) {
+      int sv[4];
+      unsigned wv4[4];
+#pragma unroll
+      for (int rx = 0; rx < 4; ++rx) {
+        const int r = r0 + ry, c = c0 + rx, i = ry + 1, j = rx + 1;
+        int state = WSHED;
+        unsigned w4 = 0;
+        if (r < H && c < W) {
+          const int wl = (c >= 1) ? cdiffp(px[i][j], px[i][j - 1]) : 0;
+          const int wr = (c + 1 < W) ? cdiffp(px[i][j], px[i][j + 1]) : 0;
+          const int wu = (r >= 1) ? cdiffp(px[i][j], px[i - 1][j]) : 0;
+          const int wd = (r + 1 < H) ? cdiffp(px[i][j], px[i + 1][j]) : 0;
+          w4 = (unsigned)wl | ((unsigned)wr << 8) | ((unsigned)wu << 16) | ((unsigned)wd << 24);
+          if (!(r == 0 || r == H - 1 || c == 0 || c == W - 1)) {
+            const int m = mv[ry][rx];
+            if (m > 0) {
+              state = m;
+            } else {
+              // interior neighbours (the frame is WSHED in the serial code and never counts)
+              const int wleft = (c >= 2) ? wl : -1;
+              const int wup = (r >= 2) ? wu : -1;
+              const int wr_i = (c <= W - 3) ? wr : -1;
+              const int wd_i = (r <= H - 3) ? wd : -1;
+              int lvl = 256;
+              if (wleft >= 0 && ((pos[i] >> (j - 1)) & 1u)) lvl = min(lvl, wleft);
+              if (wr_i >= 0 && ((pos[i] >> (j + 1)) & 1u)) lvl = min(lvl, wr_i);
+              if (wup >= 0 && ((pos[i - 1] >> j) & 1u)) lvl = min(lvl, wup);
+              if (wd_i >= 0 && ((pos[i + 1] >> j) & 1u)) lvl = min(lvl, wd_i);
+              if (lvl < 256) {
+                state = p1_state(lvl);
+                ++myrow[ry];
+              } else {
+                state = 0;
+              }
+              // this pixel may be queued once, at one of its distinct interior edge weights
+              if (wleft >= 0) atomicAdd(&caph[wleft], 1u);
+              if (wr_i >= 0 && wr_i != wleft) atomicAdd(&caph[wr_i], 1u);
+              if (wup >= 0 && wup != wleft && wup != wr_i) atomicAdd(&caph[wup], 1u);
+              if (wd_i >= 0 && wd_i != wleft && wd_i != wr_i && wd_i != wup) atomicAdd(&caph[wd_i], 1u);
+            }
+          }
+        }
+        sv[rx] = state;
+        wv4[rx] = w4;
+      }
+      out[2 * ry] = make_int4(sv[0], (int)wv4[0], sv[1], (int)wv4[1]);
+      out[2 * ry + 1] = make_int4(sv[2], (int)wv4[2], sv[3], (int)wv4[3]);
+    }
   }
-  if (mycount) atomicAdd(&ntot, mycount);
+#pragma unroll
+  for (int ry = 0; ry < 4; ++ry)
+    if (myrow[ry]) atomicAdd(&rowcnt[ry], myrow[ry]);
   __syncthreads();
   if (caph[tid]) atomicAdd(&ws.ctl->cap[tid], caph[tid]);
-  if (tid == 0) ws.tot[blockIdx.x] = ntot;
+  if (tid < 4 && tr * 4 + tid < H) ws.tot[(long long)(tr * 4 + tid) * ws.nseg + cs] = rowcnt[tid];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -363,43 +405,60 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
   }
 }
 
-// Ordered compaction of the phase-1 pixels (raster order) into ilist/desc + level histograms.
-__global__ __launch_bounds__(BS) void k_compact(Ws ws) {
-  __shared__ int wt[BS / 64];
-  __shared__ int run;
-  const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+// Ordered compaction of the phase-1 pixels in raster order into ilist/desc + level histograms.
+// One block per raster chunk (an RSEG-column row segment); thread = 4 consecutive pixels of the
+// row, i.e. one tile row (32 B of its tile's line).
+__global__ __launch_bounds__(256) void k_compact(Ws ws) {
+  __shared__ int wt[4];
   if (ws.ctl->bat.n == 0 || ws.ctl->bat.mode != 1) return;
-  if (tid == 0) run = 0;
-  const long long c0 = (long long)blockIdx.x * CH;
-  const int base = ws.choff[blockIdx.x];
-  for (int s = 0; s < SUB; ++s) {
-    const long long p = c0 + s * BS + tid;
-    const bool f = (p < ws.N) && ws.mk[p] == INQ;
-    if (!__syncthreads_or(f)) continue;
-    const unsigned long long bal = __ballot(f);
-    if (lane == 0) wt[wv] = __popcll(bal);
-    __syncthreads();
-    if (f) {
-      int off = run + lanes_below(bal);
-      for (int k = 0; k < wv; ++k) off += wt[k];
-      const long long k = (long long)base + off;
-      const int lv = ws.lv1[p];
-      ws.ilist[k] = (int32_t)p;
-      ws.desc[k] = make_desc((unsigned)lv, 1u, 0, 0);
-      atomicAdd(&ws.cnt[(k / CH) * NQ + lv], 1);
-    }
-    __syncthreads();
-    if (tid == 0) run += wt[0] + wt[1] + wt[2] + wt[3];
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const int r = blockIdx.x / ws.nseg, cs = blockIdx.x % ws.nseg;
+  const int c = cs * RSEG + tid * 4;
+  int lv[4] = {-1, -1, -1, -1};
+  int n = 0;
+  long long t0 = 0;
+  if (c < ws.W) {
+    t0 = tix(r, c, ws.Wt);
+    const int4 a = *reinterpret_cast<const int4*>(ws.mk + (t0 << 1));
+    const int4 b = *reinterpret_cast<const int4*>(ws.mk + (t0 << 1) + 4);
+    const int s[4] = {a.x, a.z, b.x, b.z};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c + k < ws.W && is_p1(s[k])) {
+        lv[k] = s[k] & 255;
+        ++n;
+      }
   }
+  int x = n;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wt[wv] = x;
+  __syncthreads();
+  long long k = (long long)ws.choff[blockIdx.x] + (x - n);
+  for (int w = 0; w < wv; ++w) k += wt[w];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (lv[q] < 0) continue;
+    ws.ilist[k] = (int32_t)(t0 + q);
+    ws.desc[k] = make_desc((unsigned)lv[q], 1u, 0, 0);
+    atomicAdd(&ws.cnt[(k / CH) * NQ + lv[q]], 1);
+    ++k;
+  }
+}
+
+__device__ __forceinline__ int ld_state(const Ws& ws, long long t) { return ws.mk[t << 1]; }
+__device__ __forceinline__ void st_state(const Ws& ws, long long t, int v) { ws.mk[t << 1] = v; }
+__device__ __forceinline__ unsigned ld_w4(const Ws& ws, long long t) {
+  return (unsigned)ws.mk[(t << 1) | 1];
 }
 
 __device__ __forceinline__ int fold_lab(int lab, int v) {
   return (lab == 0) ? v : (lab == v ? v : WSHED);
 }
 
-__device__ __forceinline__ long long nb_of(long long p, int d, long long W) {
-  return (d == 0) ? p - 1 : (d == 1) ? p + 1 : (d == 2) ? p - W : p + W;
-}
 
 __device__ __forceinline__ unsigned long long claim_tag(unsigned epoch, int rank) {
   return ((unsigned long long)epoch << 32) | (unsigned long long)(0xffffffffu - (unsigned)rank);
@@ -426,16 +485,15 @@ struct LItem {
 
 __device__ __forceinline__ void gather_label(const Ws& ws, const Seg* segs, int nseg, int i, int slot,
                                              LItem& it) {
-  const long long W = ws.W;
+  const int Wt = ws.Wt;
   const long long p = ws.qbuf[slot];
   it.p = p;
   it.base_lab = 0;
   it.zero_mask = 0;
-  it.wts = ws.w4[p];
-  const long long nb[4] = {p - 1, p + 1, p - W, p + W};
+  it.wts = ld_w4(ws, p);
   int v[4];
 #pragma unroll
-  for (int d = 0; d < 4; ++d) v[d] = ws.mk[nb[d]];
+  for (int d = 0; d < 4; ++d) v[d] = ld_state(ws, nb_of(p, d, Wt));
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     it.ldep[d] = -1;
@@ -452,22 +510,19 @@ __device__ __forceinline__ void gather_label(const Ws& ws, const Seg* segs, int 
 
 __device__ __forceinline__ void small_loop(const Ws& ws);
 
-// Small batches (<= SMALL_MAX) are handed to block 0's single-workgroup loop (small_loop), which
-// processes the following small batches too; every other block returns.
+// Small batches reach this kernel only right after a large one (k_claim's last block runs the
+// small_loop once nothing is left for k_scatter).
 __global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
   if (B.n == 0 || B.mode != 0 || ctl->error) return;
-  if (B.n <= SMALL_MAX) {
-    if (blockIdx.x == 0) small_loop(ws);
-    return;
-  }
   __shared__ Seg segs[NQ];
   load_segs(ctl, B, segs);
   __syncthreads();
   const int tid = threadIdx.x, lane = lane_id();
-  const unsigned long long etag = (unsigned long long)B.epoch << 32;
-  const long long W = ws.W;
+  const unsigned long long etag = (unsigned long long)B.epoch << 32;  // final label granule
+  const unsigned long long ptag = etag | (1ull << 63);                // provisional base fold
+  const int Wt = ws.Wt;
   unsigned long long* const dg = ws.diag;
   for (int base = blockIdx.x * RBS; base < B.n; base += gridDim.x * RBS) {
     const int wbase = base + (tid & ~63);
@@ -500,34 +555,56 @@ __global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
     long long t0 = 0;
     int spins = 0;
     const unsigned long long t_b = dg ? __builtin_amdgcn_s_memtime() : 0;
+    bool published = false;
     for (;;) {
-      int snap[4] = {0, 0, 0, 0};
+      int snap[4] = {0, 0, 0, 0}, sbase[4] = {0, 0, 0, 0};
       if (any_dep) {
 #pragma unroll
         for (int d = 0; d < 4; ++d)
           if ((inw_slots >> d) & 1u) {
             const int r = it.ldep[d];
-            snap[d] = __shfl(mylab, ((unsigned)(r - wbase) < 64u) ? r - wbase : lane);
+            const int src = ((unsigned)(r - wbase) < 64u) ? r - wbase : lane;
+            snap[d] = __shfl(mylab, src);
+            sbase[d] = __shfl(it.base_lab, src);
           }
       }
       if (pending) {
+        // fold the settled labels and the FINAL labels of resolved deps; a dep still pending whose
+        // base fold b (its settled neighbours) is WSHED or already in the fold is redundant: it
+        // ends as b or WSHED, and WSHED is not folded
         int lab = it.base_lab;
-        bool unknown = false;
+        int prov[4] = {0, 0, 0, 0};
+        unsigned pm = 0;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
           const int r = it.ldep[d];
           if (r < 0) continue;
-          int v;
+          int v, pb;
           if ((unsigned)(r - wbase) < 64u) {
             v = snap[d];
+            pb = sbase[d];
           } else {
             const unsigned long long g = ld_granule(&ws.tl[r]);
-            v = ((g & 0xffffffff00000000ull) == etag) ? (int)(uint32_t)g : 0;
+            const unsigned long long hi = g & 0xffffffff00000000ull;
+            v = (hi == etag) ? (int)(uint32_t)g : 0;
+            pb = (hi == ptag) ? (int)(uint32_t)g : 0;
           }
-          if (v == 0) unknown = true;
-          else if (v > 0) lab = fold_lab(lab, v);
+          if (v > 0) lab = fold_lab(lab, v);
+          else if (v == 0) {
+            prov[d] = pb;
+            pm |= 1u << d;
+          }
         }
-        if (lab == WSHED || !unknown) {
+        bool unknown = false;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          if (((pm >> d) & 1u) && prov[d] != WSHED && !(prov[d] > 0 && prov[d] == lab)) unknown = true;
+        if (unknown && lab != WSHED) {
+          if (!published && it.base_lab != 0) {  // let later items see this one's base fold
+            st_granule(&ws.tl[i], ptag | (uint32_t)it.base_lab);
+            published = true;
+          }
+        } else {
           if (lab == 0) {  // impossible for an exact queue: flag, label as WSHED
             atomicOr(&ctl->error, ERR_STATE);
             lab = WSHED;
@@ -539,7 +616,7 @@ __global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
           const unsigned long long ct = claim_tag(B.epoch, i);
 #pragma unroll
           for (int d = 0; d < 4; ++d)
-            if ((zm >> d) & 1u) atomicMax(&ws.claim[nb_of(it.p, d, W)], ct);
+            if ((zm >> d) & 1u) atomicMax(&ws.claim[nb_of(it.p, d, Wt)], ct);
           pending = false;
         }
       }
@@ -572,23 +649,23 @@ __global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
 // after the item) and the segment cut (push below a LATER segment's level: end the batch before
 // that segment), and the lowest pushed level.  No waiting: every claim of the batch was made
 // before this kernel started.
-__device__ void scan_body(const Ws& ws);
+__device__ Batch scan_body(const Ws& ws);
+__device__ void scatter_chunks(const Ws& ws, const Batch& B, int first, int stride);
 
 // Claim check + per-chunk level histograms, 1024-thread blocks.  The last block to finish (atomic
 // ticket, agent-scope fences on both sides) runs the scan itself, saving a kernel boundary per
-// iteration; when there is nothing to claim (small-loop skip, phase-1 pseudo-batch, end, error)
-// block 0 runs it alone.
+// iteration; when there is nothing to claim (end of flood, error) the blocks only take the ticket.
 __global__ __launch_bounds__(1024) void k_claim(Ws ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
-  const bool work = !(B.n == 0 || B.mode != 0 || ctl->error || ctl->skip);
+  const bool work = !(B.n == 0 || B.mode != 0 || ctl->error);
   __shared__ int hist[NQ];
   __shared__ Seg segs[NQ];
   __shared__ int s_minpush;
   if (work) load_segs(ctl, B, segs);
   if (threadIdx.x == 0) s_minpush = NQ;
   const int tid = threadIdx.x;
-  const long long W = ws.W;
+  const int Wt = ws.Wt;
   for (int base = blockIdx.x * 1024; work && base < B.n; base += gridDim.x * 1024) {
     if (tid < NQ) hist[tid] = 0;
     __syncthreads();
@@ -607,7 +684,7 @@ __global__ __launch_bounds__(1024) void k_claim(Ws ws) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           if (!((zm >> k) & 1u)) continue;
-          if (ws.claim[nb_of(p, k, W)] == ct) {
+          if (ws.claim[nb_of(p, k, Wt)] == ct) {
             push |= 1u << k;
             const int lv = (wts >> (8 * k)) & 255;
             atomicAdd(&hist[lv], 1);
@@ -649,26 +726,30 @@ __global__ __launch_bounds__(1024) void k_claim(Ws ws) {
   }
   __syncthreads();
   if (!hist[0]) return;
-  scan_body(ws);
+  const Batch cb = scan_body(ws);
+  // a committed batch of at most SMALL_MAX items is scattered here; then, with nothing left for
+  // k_scatter, this block runs the following small batches itself (small_loop)
+  if (cb.nchunk > 0 && cb.n <= SMALL_MAX && !ctl->error) {
+    scatter_chunks(ws, cb, 0, 1);
+    __syncthreads();
+    if (tid == 0) ctl->cbat.nchunk = 0;
+  } else if (cb.nchunk > 0) {
+    return;  // k_scatter commits it
+  }
+  small_loop(ws);
 }
 
 // ---------------------------------------------------------------------------------------------
 // Scan (1 block x 1024): committed prefix (interrupt cut, segment cut), recount of the cut chunk,
 // column scan -> per-chunk bucket offsets, head/tail update, hand the committed batch to k_scatter
 // (cbat), form the next batch.
-__device__ void scan_body(const Ws& ws) {
+__device__ Batch scan_body(const Ws& ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
   const int tid = threadIdx.x;
-  if (ctl->skip) {  // k_resolve ran small batches and left an unresolved large one: next iteration
-    __syncthreads();
-    if (tid == 0) {
-      ctl->skip = 0;
-      ctl->cbat.n = 0;
-      ctl->cbat.nchunk = 0;
-    }
-    return;
-  }
+  Batch none = B;
+  none.n = 0;
+  none.nchunk = 0;
   if (B.n == 0 || ctl->error) {  // nothing committed this iteration (finished, or stopped)
     __syncthreads();
     if (tid == 0) {
@@ -679,7 +760,7 @@ __device__ void scan_body(const Ws& ws) {
         ctl->done = 1;
       }
     }
-    return;
+    return none;
   }
   // the queue state lives in LDS for the whole kernel: one parallel load, one write-back
   __shared__ int partial[NQ];
@@ -687,6 +768,7 @@ __device__ void scan_body(const Ws& ws) {
   __shared__ Seg s_seg[NQ];
   __shared__ Seg nsegs[NQ];
   __shared__ int s_nseg, s_n;
+  __shared__ Batch s_cb;
   if (tid < NQ) {
     s_head[tid] = ctl->qhead[tid];
     s_tail[tid] = ctl->qtail[tid];
@@ -729,6 +811,7 @@ __device__ void scan_body(const Ws& ws) {
     cb.ncommit = ncommit;
     cb.nchunk = nch;
     ctl->cbat = cb;
+    s_cb = cb;
   }
   // the histogram rows this batch accumulated are zeroed by k_scatter (cbat.n covers them all)
   __syncthreads();
@@ -759,6 +842,7 @@ __device__ void scan_body(const Ws& ws) {
   }
   const int q = block_sum(tid < NQ ? s_tail[tid] - s_head[tid] : 0);
   if (tid == 0) ctl->remaining = q;
+  return s_cb;  // block_sum's barriers made s_cb visible
 }
 
 __global__ __launch_bounds__(1024) void k_scan(Ws ws) { scan_body(ws); }
@@ -802,23 +886,21 @@ __device__ __forceinline__ void wave_rank(unsigned mask, unsigned lvls, int pos[
 // sub-round's in-chunk offset is the chunk offset (k_scan) plus the per-level push counts of the
 // chunk's earlier sub-rounds, recounted here from their (L2-resident) descriptors.  The blocks
 // also zero the histogram rows the batch accumulated (consumed by k_scan).
-__global__ __launch_bounds__(1024) void k_scatter(Ws ws) {
+__device__ void scatter_chunks(const Ws& ws, const Batch& B, int first, int stride) {
   Ctl* ctl = ws.ctl;
-  const Batch B = ctl->cbat;
-  if (B.nchunk == 0 || ctl->error) return;
   constexpr int NW = 16, SUBS = CH / 1024;
   __shared__ int run[NQ];
   __shared__ int wcnt[NW][NQ];
   __shared__ int qb[NQ];
   const int tid = threadIdx.x, wv = tid >> 6;
-  const long long W = ws.W;
+  const int Wt = ws.Wt;
   {
     const long long rows = (long long)((B.n + CH - 1) / CH) * NQ;
-    for (long long k = (long long)blockIdx.x * 1024 + tid; k < rows; k += (long long)gridDim.x * 1024)
+    for (long long k = (long long)first * 1024 + tid; k < rows; k += (long long)stride * 1024)
       ws.cnt[k] = 0;
   }
   if (tid < NQ) qb[tid] = ctl->qbase[tid];
-  for (int vb = blockIdx.x; vb < B.nchunk * SUBS; vb += gridDim.x) {
+  for (int vb = first; vb < B.nchunk * SUBS; vb += stride) {
     const int ch = vb / SUBS, i0 = ch * CH + (vb % SUBS) * 1024;
     if (i0 >= B.ncommit) continue;  // block-uniform
     if (tid < NQ) {
@@ -844,7 +926,7 @@ __global__ __launch_bounds__(1024) void k_scatter(Ws ws) {
       lvls = (unsigned)d;
       if (B.mode == 0) {
         p = ws.ipx[i];
-        ws.mk[p] = (int32_t)(uint32_t)ws.tl[i];
+        st_state(ws, p, (int32_t)(uint32_t)ws.tl[i]);
       } else {
         p = ws.ilist[i];
       }
@@ -871,12 +953,18 @@ __global__ __launch_bounds__(1024) void k_scatter(Ws ws) {
         atomicOr(&ctl->error, ERR_CAPACITY);
         continue;
       }
-      const long long n = (B.mode == 0) ? nb_of(p, d, W) : p;
-      ws.mk[n] = queued_state(dest);
+      const long long n = (B.mode == 0) ? nb_of(p, d, Wt) : p;
+      st_state(ws, n, queued_state(dest));
       ws.qbuf[dest] = (int32_t)n;
     }
     __syncthreads();  // before the next sub-round reuses run/wcnt
   }
+}
+
+__global__ __launch_bounds__(1024) void k_scatter(Ws ws) {
+  const Batch B = ws.ctl->cbat;
+  if (B.nchunk == 0 || ws.ctl->error) return;
+  scatter_chunks(ws, B, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -896,18 +984,21 @@ struct Item {
 
 __device__ __forceinline__ void gather_item(const Ws& ws, const Seg* segs, int nseg, int i, int slot,
                                             Item& it) {
-  const long long W = ws.W;
+  const int Wt = ws.Wt;
   const long long p = ws.qbuf[slot];
   it.p = p;
   it.base_lab = 0;
   it.zero_mask = 0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) it.dep[k] = -1;
-  it.wts = ws.w4[p];
-  const long long nb[4] = {p - 1, p + 1, p - W, p + W};
+  it.wts = ld_w4(ws, p);
+  long long nb[4];
   int v[4];
 #pragma unroll
-  for (int d = 0; d < 4; ++d) v[d] = ws.mk[nb[d]];
+  for (int d = 0; d < 4; ++d) {
+    nb[d] = nb_of(p, d, Wt);
+    v[d] = ld_state(ws, nb[d]);
+  }
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     if (v[d] > 0) {
@@ -924,14 +1015,14 @@ __device__ __forceinline__ void gather_item(const Ws& ws, const Seg* segs, int n
   for (int d = 0; d < 4; ++d) {
     if (!((it.zero_mask >> d) & 1u)) continue;
     const long long n = nb[d];
-    // n's neighbours other than p (p is n's opposite-direction neighbour)
-    const long long o0 = (d == 0) ? n - 1 : (d == 1) ? n + 1 : n - 1;
-    const long long o1 = (d <= 1) ? n - W : n + 1;
-    const long long o2 = (d == 0 || d == 1) ? n + W : (d == 2) ? n - W : n + W;
-    const long long o[3] = {o0, o1, o2};
+    // n's neighbours other than p (p is n's opposite-direction neighbour), directions ascending
+    const int e0 = (d == 1) ? 1 : 0;
+    const int e1 = (d <= 1) ? 2 : 1;
+    const int e2 = (d == 2) ? 2 : 3;
+    const long long o[3] = {nb_of(n, e0, Wt), nb_of(n, e1, Wt), nb_of(n, e2, Wt)};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const int vo = ws.mk[o[k]];
+      const int vo = ld_state(ws, o[k]);
       if (vo <= -3) {
         const int r = rank_of_slot(segs, nseg, state_slot(vo));
         if (r >= 0 && r < i) it.dep[4 + 3 * d + k] = r;
@@ -995,7 +1086,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
   __shared__ int s_cut, s_segcut, s_minpush, s_err, s_nseg, s_n;
   __shared__ Batch s_B;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-  const long long W = ws.W;
+  const int Wt = ws.Wt;
   if (tid == 0) {
     s_B = ctl->bat;
     s_err = ctl->error;
@@ -1104,7 +1195,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
         lvls = (unsigned)d;
         const int sg = (int)((d >> 48) & 255);
         p = ws.qbuf[s_seg[sg].bstart + (i - s_seg[sg].rank)];
-        ws.mk[p] = vlab[i];
+        st_state(ws, p, vlab[i]);
       }
       int pos[4] = {0, 0, 0, 0};
       wave_rank(mask, lvls, pos, s_wcnt[wv]);
@@ -1129,8 +1220,8 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
           s_err = ERR_CAPACITY;
           continue;
         }
-        const long long n = nb_of(p, d, W);
-        ws.mk[n] = queued_state(dest);
+        const long long n = nb_of(p, d, Wt);
+        st_state(ws, n, queued_state(dest));
         ws.qbuf[dest] = (int32_t)n;
         ++pushed;
       }
@@ -1196,9 +1287,6 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     ctl->pushes += nb_push;
     if (s_err) ctl->error |= s_err;
     if (s_B.n == 0 && !s_err) ctl->done = 1;
-    // the next batch is large and has not been resolved in this launch: the rest of this
-    // iteration (k_claim, k_scan, k_scatter) must not touch it
-    if (s_B.n > 0) ctl->skip = 1;
   }
 }
 
@@ -1267,6 +1355,81 @@ __global__ __launch_bounds__(256) void k_colorize(const int32_t* __restrict__ la
       }
       if (cnt == 4 && (q & 3) == 0) *reinterpret_cast<uint32_t*>(gray + q) = g4;
       else for (int k = 0; k < cnt; ++k) gray[q + k] = (g4 >> (8 * k)) & 255;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// End of the flood: tiled states -> the caller's row-major label map (cv::watershed's in-place
+// markers), fused with colorByIndexes (PictureService.java:913-936) + optional BGR2GRAY when dst
+// is given.  One thread = one 4x4 tile: one 128-B line in, four 16-B label rows out.
+__device__ __forceinline__ uint32_t label_colour(int x, int depth, const uint8_t* pal, bool lds_pal,
+                                                 const uint32_t* spal) {
+  if (x <= 0 || x > depth) return 0;
+  if (pal == nullptr) return 0xffffffu;
+  if (lds_pal) return spal[x - 1];
+  return (uint32_t)pal[3 * (x - 1)] | ((uint32_t)pal[3 * (x - 1) + 1] << 8) |
+         ((uint32_t)pal[3 * (x - 1) + 2] << 16);
+}
+
+__global__ __launch_bounds__(256) void k_untile(const int32_t* __restrict__ mk, int H, int W, int Wt,
+                                                int32_t* __restrict__ lab, int depth,
+                                                const uint8_t* __restrict__ pal,
+                                                uint8_t* __restrict__ dst, uint8_t* __restrict__ gray) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t spal[];
+  const bool lds_pal = dst != nullptr && pal != nullptr && depth <= PAL_LDS_MAX;
+  if (lds_pal) {
+    for (int k = threadIdx.x; k < depth; k += blockDim.x)
+      spal[k] = (uint32_t)pal[3 * k] | ((uint32_t)pal[3 * k + 1] << 8) | ((uint32_t)pal[3 * k + 2] << 16);
+    __syncthreads();
+  }
+  const long long ntiles = (long long)((H + 3) >> 2) * Wt;
+  const bool vec = (W & 3) == 0 && (((uintptr_t)lab) & 15) == 0;
+  const bool vec3 = (W & 3) == 0 && dst != nullptr && (((uintptr_t)dst) & 3) == 0;
+  const bool vecg = (W & 3) == 0 && gray != nullptr && (((uintptr_t)gray) & 3) == 0;
+  for (long long tt = (long long)blockIdx.x * blockDim.x + threadIdx.x; tt < ntiles;
+       tt += (long long)gridDim.x * blockDim.x) {
+    const int r0 = (int)(tt / Wt) * 4, c0 = (int)(tt % Wt) * 4;
+    const int4* src = reinterpret_cast<const int4*>(mk + (tt << 5));
+#pragma unroll
+    for (int ry = 0; ry < 4; ++ry) {
+      const int r = r0 + ry;
+      if (r >= H) break;
+      const int4 a = src[2 * ry], b = src[2 * ry + 1];
+      const int l[4] = {a.x, a.z, b.x, b.z};
+      const long long q = (long long)r * W + c0;
+      const bool full = c0 + 4 <= W;
+      if (full && vec) {
+        *reinterpret_cast<int4*>(lab + q) = make_int4(l[0], l[1], l[2], l[3]);
+      } else {
+        for (int k = 0; k < 4 && c0 + k < W; ++k) lab[q + k] = l[k];
+      }
+      if (dst == nullptr) continue;
+      uint32_t col[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) col[k] = label_colour(l[k], depth, pal, lds_pal, spal);
+      uint8_t* o = dst + q * 3;
+      if (full && vec3) {  // 12 bytes: B0G0R0B1 G1R1B2G2 R2B3G3R3
+        reinterpret_cast<uint32_t*>(o)[0] = (col[0] & 0xffffffu) | (col[1] << 24);
+        reinterpret_cast<uint32_t*>(o)[1] = ((col[1] >> 8) & 0xffffu) | (col[2] << 16);
+        reinterpret_cast<uint32_t*>(o)[2] = ((col[2] >> 16) & 0xffu) | (col[3] << 8);
+      } else {
+        for (int k = 0; k < 4 && c0 + k < W; ++k) {
+          o[3 * k] = col[k] & 255;
+          o[3 * k + 1] = (col[k] >> 8) & 255;
+          o[3 * k + 2] = (col[k] >> 16) & 255;
+        }
+      }
+      if (gray) {
+        uint32_t g4 = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t bb = col[k] & 255, gg = (col[k] >> 8) & 255, rr = (col[k] >> 16) & 255;
+          g4 |= ((1868u * bb + 9617u * gg + 4899u * rr + 8192u) >> 14) << (8 * k);
+        }
+        if (full && vecg) *reinterpret_cast<uint32_t*>(gray + q) = g4;
+        else for (int k = 0; k < 4 && c0 + k < W; ++k) gray[q + k] = (g4 >> (8 * k)) & 255;
+      }
     }
   }
 }

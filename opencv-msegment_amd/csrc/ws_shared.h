@@ -22,6 +22,27 @@ constexpr int PAL_LDS_MAX = 16384; // palettes up to this many labels are staged
 constexpr int MERGE_CAP = 1 << 22; // largest multi-segment batch (items)
 constexpr long long SPIN_LIMIT_TICKS = 200000000ll;  // 2 s of s_memrealtime (100 MHz)
 
+// Per-pixel flood state is TILED: 4x4-pixel tiles of 8-byte {state, w4} words (128 B = one L2
+// line per tile), tiles row-major, Wt tiles per tile row.  A pixel and its 4 neighbours mostly
+// share a line, so a queue item costs ~2 random lines instead of ~4.
+constexpr int RSEG = 1024;  // columns per raster chunk of the phase-1 compaction (256 tiles)
+__host__ __device__ inline long long tix(int r, int c, int Wt) {
+  return ((long long)((long long)(r >> 2) * Wt + (c >> 2)) << 4) | ((r & 3) << 2) | (c & 3);
+}
+// neighbour of tiled pixel t in direction d (0 left, 1 right, 2 up, 3 down); must exist
+__host__ __device__ inline long long nb_of(long long t, int d, int Wt) {
+  const long long row = (long long)Wt << 4;
+  switch (d) {
+    case 0: return (t & 3) ? t - 1 : t - 13;
+    case 1: return ((t & 3) != 3) ? t + 1 : t + 13;
+    case 2: return (t & 12) ? t - 4 : t - row + 12;
+    default: return ((t & 12) != 12) ? t + 4 : t + row - 12;
+  }
+}
+// phase-1 marker (k_prep -> k_compact): IN_QUEUE with its initial level lv
+__host__ __device__ inline int p1_state(int lv) { return (int)(0x80000000u | (unsigned)lv); }
+__host__ __device__ inline bool is_p1(int s) { return ((unsigned)s ^ 0x80000000u) < 256u; }
+
 constexpr int ERR_TIMEOUT = 1;
 constexpr int ERR_STATE = 2;
 constexpr int ERR_CAPACITY = 4;
@@ -63,7 +84,6 @@ struct Ctl {
   int cut;      // first rank of the current batch that pushes below its own level (NONE: none)
   int segcut;   // first segment invalidated by a push below its level (NONE: none)
   int minpush;  // lowest level pushed by the current batch (merge heuristic)
-  int skip;     // k_resolve ran small batches and left a large one unresolved: skip this iteration
   unsigned ticket;  // k_claim blocks finished this iteration (the last one runs the scan)
   int done;
   int error;
@@ -76,22 +96,22 @@ struct Ctl {
 
 struct Ws {
   const uint8_t* img;
-  int32_t* mk;       // label state; a queued pixel holds queued_state(slot) = -3 - slot
-  uint32_t* w4;      // 4 packed 8-bit L-inf distances to the L,R,T,B neighbours
-  uint8_t* lv1;
-  int32_t* qbuf;
+  int32_t* mk;       // TILED pixel words (see tix): state at mk[2t], 4 packed weights at mk[2t+1]
+  int32_t* qbuf;     // bucket regions of tiled pixel indices
   int32_t* ilist;
   unsigned long long* tl;
   unsigned long long* desc;
-  unsigned long long* claim;  // per-pixel {epoch, ~rank} push claims (k_resolve -> k_claim)
+  unsigned long long* claim;  // per tiled pixel {epoch, ~rank} push claims (k_resolve -> k_claim)
   int32_t* ipx;      // pixel of each rank of the current batch (k_resolve -> k_claim, k_scatter)
   int32_t* cnt;
   int32_t* coff;
-  int32_t* tot;
+  int32_t* tot;      // phase-1 pixels per raster chunk (k_prep -> k_init_scan)
   int32_t* choff;
   Ctl* ctl;
   unsigned long long* diag;  // nullptr = off; else 8 counters (msg_set_diag)
   int H, W;
+  int Wt;            // tiles per tile row = ceil(W / 4)
+  int nseg;          // raster chunks per image row = ceil(W / RSEG)
   long long N;
   long long qcap;
 };
