@@ -32,7 +32,8 @@ struct msg_ctx {
   int32_t* d_px = nullptr;  // tiled {state, w4} words
   int32_t *d_qbuf = nullptr, *d_ilist = nullptr;
   int32_t *d_cnt = nullptr, *d_coff = nullptr, *d_tot = nullptr, *d_choff = nullptr;
-  unsigned long long *d_tl = nullptr, *d_desc = nullptr, *d_claim = nullptr;
+  unsigned* d_capp = nullptr;  // CAP_SLOTS x NQ
+  unsigned long long *d_tl = nullptr, *d_desc = nullptr;
   long long qcap = 0;
   // staging for the host-buffer entry points
   long long stage_n = 0;
@@ -134,8 +135,8 @@ void dfree(T*& p) {
 void free_flood(msg_ctx* c) {
   dfree(c->d_px);
   dfree(c->d_qbuf); dfree(c->d_ilist);
-  dfree(c->d_cnt); dfree(c->d_coff); dfree(c->d_tot); dfree(c->d_choff);
-  dfree(c->d_tl); dfree(c->d_desc); dfree(c->d_claim);
+  dfree(c->d_cnt); dfree(c->d_coff); dfree(c->d_tot); dfree(c->d_choff); dfree(c->d_capp);
+  dfree(c->d_tl); dfree(c->d_desc);
   c->cap_n = c->cap_np = c->cap_rc = 0;
   c->qcap = 0;
 }
@@ -163,9 +164,8 @@ int ensure_flood(msg_ctx* c, int H, int W) {
   HIPCHK(c, hipMalloc((void**)&c->d_coff, nch * NQ * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_tot, rc * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_choff, rc * 4));
-  HIPCHK(c, hipMalloc((void**)&c->d_claim, np * 8));
+  HIPCHK(c, hipMalloc((void**)&c->d_capp, (size_t)CAP_SLOTS * NQ * 4));
   HIPCHK(c, hipMemset(c->d_tl, 0, n * 8));
-  HIPCHK(c, hipMemset(c->d_claim, 0, np * 8));
   c->epoch = 1;
   c->cap_n = n;
   c->cap_np = np;
@@ -206,7 +206,6 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   if (rc) return rc;
   if (c->epoch > 0x70000000u) {  // granule bit 63 flags a provisional value
     HIPCHK(c, hipMemsetAsync(c->d_tl, 0, c->cap_n * 8, st));
-    HIPCHK(c, hipMemsetAsync(c->d_claim, 0, c->cap_np * 8, st));
     c->epoch = 1;
   }
   Ws ws;
@@ -216,12 +215,12 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   ws.ilist = c->d_ilist;
   ws.tl = c->d_tl;
   ws.desc = c->d_desc;
-  ws.claim = c->d_claim;
   ws.ipx = c->d_ilist;
   ws.cnt = c->d_cnt;
   ws.coff = c->d_coff;
   ws.tot = c->d_tot;
   ws.choff = c->d_choff;
+  ws.capp = c->d_capp;
   ws.ctl = c->d_ctl;
   ws.diag = c->diag ? c->d_diag : nullptr;
   ws.H = H;
@@ -233,15 +232,15 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
 
   const int npx = (int)((N + CH - 1) / CH);
   const int gres = std::max(1, std::min(c->res_grid, (int)((N + RBS - 1) / RBS)));
-  const int gclaim = std::min(npx * (CH / 1024), 256);
   const int gsc = std::min(npx * (CH / 1024), 1024);
   HIPCHK(c, hipMemsetAsync(c->d_ctl, 0, sizeof(Ctl), st));
+  HIPCHK(c, hipMemsetAsync(c->d_capp, 0, (size_t)CAP_SLOTS * NQ * 4, st));
   if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 8 * sizeof(unsigned long long), st));
   HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)npx * NQ * sizeof(int32_t), st));
   const int nrc = H * ws.nseg;  // raster chunks
   LAUNCH(c, KID_PREP, st, k_prep, dim3((H + 3) / 4 * ws.nseg), dim3(256), 0, ws, d_mk_in);
   LAUNCH(c, KID_INIT_SCAN, st, k_init_scan, dim3(1), dim3(1024), 0, ws, nrc, c->epoch);
-  LAUNCH(c, KID_COMPACT, st, k_compact, dim3(nrc), dim3(256), 0, ws);
+  LAUNCH(c, KID_COMPACT, st, k_compact, dim3((nrc + 3) / 4), dim3(256), 0, ws, nrc);
   LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
   LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws);
   HIPCHK(c, hipGetLastError());
@@ -251,8 +250,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   long long syncs = 0;
   for (;;) {
     for (int g = 0; g < c->group; ++g, ++it) {
-      LAUNCH(c, KID_RESOLVE, st, k_resolve, dim3(gres), dim3(RBS), 0, ws);
-      LAUNCH(c, KID_CLAIM, st, k_claim, dim3(gclaim), dim3(1024), 0, ws);  // + scan (last block)
+      LAUNCH(c, KID_RESOLVE, st, k_resolve, dim3(gres), dim3(RBS), 0, ws);  // + scan (last block)
       LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws);
     }
     HIPCHK(c, hipGetLastError());
@@ -275,8 +273,8 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
     slot ^= 1;
   }
   {
-    const long long ntiles = (long long)((H + 3) / 4) * ws.Wt;
-    const int grid = (int)std::min<long long>((ntiles + 255) / 256, 4096);
+    const long long nunits = (long long)((H + 3) / 4) * ws.Wt * 8;
+    const int grid = (int)std::min<long long>((nunits + 255) / 256, 8192);
     const size_t shm = (d_dst && d_pal && depth <= PAL_LDS_MAX) ? (size_t)std::max(depth, 1) * 4 : 0;
     LAUNCH(c, KID_UNTILE, st, k_untile, dim3(grid), dim3(256), shm, c->d_px, H, W, ws.Wt, d_labels,
            depth, d_pal, d_dst, d_gray);

@@ -88,36 +88,101 @@ __device__ __forceinline__ int cdiffp(uint32_t a, uint32_t b) {  // L-inf BGR di
   return max(max(d0, d1), d2);
 }
 
+constexpr int PREP_COLS = RSEG + 2;                 // strip columns incl. the 1-pixel halo
+constexpr int PREP_RAW = (3 * PREP_COLS + 8) / 4 + 1; // dwords of one BGR row segment
+
 __global__ __launch_bounds__(256) void k_prep(Ws ws, const int32_t* __restrict__ mk_in) {
   static_assert(NQ == 256 && RSEG == 1024, "one thread per level and per tile of the strip");
   __shared__ unsigned caph[NQ];
-  __shared__ int rowcnt[4];
-  const int tid = threadIdx.x;
-  caph[tid] = 0;
-  if (tid < 4) rowcnt[tid] = 0;
-  __syncthreads();
+  __shared__ uint32_t s_raw[6][PREP_RAW];
+  __shared__ uint32_t s_px[6][PREP_COLS];
+  __shared__ int32_t s_m[6][PREP_COLS];
+  __shared__ unsigned long long s_wsum[4];
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const int H = ws.H, W = ws.W, Wt = ws.Wt;
   const int tr = blockIdx.x / ws.nseg, cs = blockIdx.x % ws.nseg;
-  const int tc = cs * (RSEG / 4) + tid;
-  int myrow[4] = {0, 0, 0, 0};
-  if (tc < Wt) {
-    const int r0 = tr * 4, c0 = tc * 4;
-    uint32_t px[6][6];  // colours of rows r0-1..r0+4, cols c0-1..c0+4 (0 outside the image)
-    unsigned pos[6];    // bit j: marker > 0 at (r0-1+i, c0-1+j)
-    int mv[4][4];
+  const int r0 = tr * 4, x0 = cs * RSEG;
+  const int ncol = min(RSEG, W - x0) + 2;  // strip column j <-> image column x0 - 1 + j
+  const long long nbytes = 3ll * H * W;
+  caph[tid] = 0;
+  // ---- stage rows r0-1..r0+4 of the strip: markers as ints, BGR as aligned dwords; every load
+  // is issued into registers before the first LDS store (54 independent loads in flight) ----
+  const bool aligned = (((uintptr_t)ws.img) & 3) == 0;
+  long long a0[6];
+  int mreg[6][5];
+  uint32_t ireg[6][4];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      pos[i] = 0;
+  for (int i = 0; i < 6; ++i) {
+    const int r = r0 - 1 + i;
+    const bool rin = r >= 0 && r < H;
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const int r = r0 - 1 + i, c = c0 - 1 + j;
-        px[i][j] = ld_bgr(ws.img, r, c, H, W);
-        const bool in = r >= 0 && r < H && c >= 0 && c < W;
-        const int m = in ? mk_in[(long long)r * W + c] : 0;
-        if (m > 0) pos[i] |= 1u << j;
-        if (i >= 1 && i <= 4 && j >= 1 && j <= 4) mv[i - 1][j - 1] = m;
-      }
+    for (int it = 0; it < 5; ++it) {
+      const int j = tid + 256 * it, c = x0 - 1 + j;
+      mreg[i][it] = (rin && j < ncol && c >= 0 && c < W) ? mk_in[(long long)r * W + c] : 0;
     }
+    const int ca = max(x0 - 1, 0), cb = min(x0 + ncol - 1, W);
+    a0[i] = (3ll * ((long long)r * W + ca)) & ~3ll;
+    const long long e = rin ? 3ll * ((long long)r * W + cb) : a0[i];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const long long ad = a0[i] + 4ll * (tid + 256 * it);
+      uint32_t w = 0;
+      if (ad < e) {
+        if (aligned && ad + 4 <= nbytes) {
+          w = *reinterpret_cast<const uint32_t*>(ws.img + ad);
+        } else {
+          for (int k = 0; k < 4; ++k)
+            if (ad + k < nbytes) w |= (uint32_t)ws.img[ad + k] << (8 * k);
+        }
+      }
+      ireg[i][it] = w;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+#pragma unroll
+    for (int it = 0; it < 5; ++it) {
+      const int j = tid + 256 * it;
+      if (j < ncol) s_m[i][j] = mreg[i][it];
+    }
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int q = tid + 256 * it;
+      if (q < PREP_RAW) s_raw[i][q] = ireg[i][it];
+    }
+  }
+  __syncthreads();
+  const uint8_t* rawb = reinterpret_cast<const uint8_t*>(&s_raw[0][0]);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int r = r0 - 1 + i;
+    for (int j = tid; j < ncol; j += 256) {
+      const int c = x0 - 1 + j;
+      uint32_t v = 0;
+      if (r >= 0 && r < H && c >= 0 && c < W) {
+        const int o = (int)(3ll * ((long long)r * W + c) - a0[i]) + i * PREP_RAW * 4;
+        v = (uint32_t)rawb[o] | ((uint32_t)rawb[o + 1] << 8) | ((uint32_t)rawb[o + 2] << 16);
+      }
+      s_px[i][j] = v;
+    }
+  }
+  __syncthreads();
+  // ---- one tile per thread ----
+  const int tc = cs * (RSEG / 4) + tid;
+  int run_w = -1;
+  unsigned run_n = 0;
+  auto cap_add = [&](int w) {
+    if (w != run_w) {
+      if (run_n) atomicAdd(&caph[run_w], run_n);
+      run_w = w;
+      run_n = 0;
+    }
+    ++run_n;
+  };
+  unsigned p1mask = 0;            // bit 4*ry+rx: phase-1 pixel
+  unsigned long long rows4 = 0;   // 16-bit phase-1 counts of the 4 tile rows
+  if (tc < Wt) {
+    const int c0 = tc * 4, jb = 4 * tid;  // strip column of c0 - 1
     int4* out = reinterpret_cast<int4*>(ws.mk + ((((long long)tr * Wt + tc) << 4) << 1));
 #pragma unroll
     for (int ry = 0; ry < 4; ++ry) {
@@ -125,17 +190,18 @@ __global__ __launch_bounds__(256) void k_prep(Ws ws, const int32_t* __restrict__
       unsigned wv4[4];
 #pragma unroll
       for (int rx = 0; rx < 4; ++rx) {
-        const int r = r0 + ry, c = c0 + rx, i = ry + 1, j = rx + 1;
+        const int r = r0 + ry, c = c0 + rx, i = ry + 1, j = jb + rx + 1;
         int state = WSHED;
         unsigned w4 = 0;
         if (r < H && c < W) {
-          const int wl = (c >= 1) ? cdiffp(px[i][j], px[i][j - 1]) : 0;
-          const int wr = (c + 1 < W) ? cdiffp(px[i][j], px[i][j + 1]) : 0;
-          const int wu = (r >= 1) ? cdiffp(px[i][j], px[i - 1][j]) : 0;
-          const int wd = (r + 1 < H) ? cdiffp(px[i][j], px[i + 1][j]) : 0;
+          const uint32_t me = s_px[i][j];
+          const int wl = (c >= 1) ? cdiffp(me, s_px[i][j - 1]) : 0;
+          const int wr = (c + 1 < W) ? cdiffp(me, s_px[i][j + 1]) : 0;
+          const int wu = (r >= 1) ? cdiffp(me, s_px[i - 1][j]) : 0;
+          const int wd = (r + 1 < H) ? cdiffp(me, s_px[i + 1][j]) : 0;
           w4 = (unsigned)wl | ((unsigned)wr << 8) | ((unsigned)wu << 16) | ((unsigned)wd << 24);
           if (!(r == 0 || r == H - 1 || c == 0 || c == W - 1)) {
-            const int m = mv[ry][rx];
+            const int m = s_m[i][j];
             if (m > 0) {
               state = m;
             } else {
@@ -145,21 +211,23 @@ __global__ __launch_bounds__(256) void k_prep(Ws ws, const int32_t* __restrict__
               const int wr_i = (c <= W - 3) ? wr : -1;
               const int wd_i = (r <= H - 3) ? wd : -1;
               int lvl = 256;
-              if (wleft >= 0 && ((pos[i] >> (j - 1)) & 1u)) lvl = min(lvl, wleft);
-              if (wr_i >= 0 && ((pos[i] >> (j + 1)) & 1u)) lvl = min(lvl, wr_i);
-              if (wup >= 0 && ((pos[i - 1] >> j) & 1u)) lvl = min(lvl, wup);
-              if (wd_i >= 0 && ((pos[i + 1] >> j) & 1u)) lvl = min(lvl, wd_i);
+              if (wleft >= 0 && s_m[i][j - 1] > 0) lvl = min(lvl, wleft);
+              if (wr_i >= 0 && s_m[i][j + 1] > 0) lvl = min(lvl, wr_i);
+              if (wup >= 0 && s_m[i - 1][j] > 0) lvl = min(lvl, wup);
+              if (wd_i >= 0 && s_m[i + 1][j] > 0) lvl = min(lvl, wd_i);
               if (lvl < 256) {
                 state = p1_state(lvl);
-                ++myrow[ry];
+                p1mask |= 1u << (4 * ry + rx);
+                rows4 += 1ull << (16 * ry);
               } else {
                 state = 0;
               }
-              // this pixel may be queued once, at one of its distinct interior edge weights
-              if (wleft >= 0) atomicAdd(&caph[wleft], 1u);
-              if (wr_i >= 0 && wr_i != wleft) atomicAdd(&caph[wr_i], 1u);
-              if (wup >= 0 && wup != wleft && wup != wr_i) atomicAdd(&caph[wup], 1u);
-              if (wd_i >= 0 && wd_i != wleft && wd_i != wr_i && wd_i != wup) atomicAdd(&caph[wd_i], 1u);
+              // this pixel may be queued once, at one of its distinct interior edge weights;
+              // run-length counted in registers (plateaus: one LDS atomic per thread, not per pixel)
+              if (wleft >= 0) cap_add(wleft);
+              if (wr_i >= 0 && wr_i != wleft) cap_add(wr_i);
+              if (wup >= 0 && wup != wleft && wup != wr_i) cap_add(wup);
+              if (wd_i >= 0 && wd_i != wleft && wd_i != wr_i && wd_i != wup) cap_add(wd_i);
             }
           }
         }
@@ -170,12 +238,33 @@ __global__ __launch_bounds__(256) void k_prep(Ws ws, const int32_t* __restrict__
       out[2 * ry + 1] = make_int4(sv[2], (int)wv4[2], sv[3], (int)wv4[3]);
     }
   }
+  if (run_n) atomicAdd(&caph[run_w], run_n);
+  // ---- phase-1 pixels of each of the 4 raster chunks, in raster order, into scratch at the
+  // chunk's raster offset in qbuf (read by k_compact; qbuf is filled only after it) ----
+  unsigned long long x = rows4;
 #pragma unroll
-  for (int ry = 0; ry < 4; ++ry)
-    if (myrow[ry]) atomicAdd(&rowcnt[ry], myrow[ry]);
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_wsum[wv] = x;
   __syncthreads();
-  if (caph[tid]) atomicAdd(&ws.ctl->cap[tid], caph[tid]);
-  if (tid < 4 && tr * 4 + tid < H) ws.tot[(long long)(tr * 4 + tid) * ws.nseg + cs] = rowcnt[tid];
+  unsigned long long excl = x - rows4;
+  for (int k = 0; k < wv; ++k) excl += s_wsum[k];
+  const unsigned long long total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+  if (p1mask) {
+    const long long t0 = ((long long)tr * Wt + tc) << 4;
+#pragma unroll
+    for (int ry = 0; ry < 4; ++ry) {
+      long long q = (long long)(r0 + ry) * W + x0 + (long long)((excl >> (16 * ry)) & 0xffff);
+#pragma unroll
+      for (int rx = 0; rx < 4; ++rx)
+        if ((p1mask >> (4 * ry + rx)) & 1u) ws.qbuf[q++] = (int32_t)(t0 + 4 * ry + rx);
+    }
+  }
+  if (caph[tid]) atomicAdd(&ws.capp[(blockIdx.x % CAP_SLOTS) * NQ + tid], caph[tid]);
+  if (tid < 4 && r0 + tid < H)
+    ws.tot[(long long)(r0 + tid) * ws.nseg + cs] = (int)((total >> (16 * tid)) & 0xffff);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -349,20 +438,51 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
   Ctl* ctl = ws.ctl;
   const int tid = threadIdx.x;
   __shared__ long long wsum[16];
+  __shared__ long long capw[4];
   __shared__ long long total_items;
-  if (tid == 0) {
-    long long acc = 0;
-    for (int l = 0; l < NQ; ++l) {
-      ctl->qbase[l] = (int)acc;
-      acc += ctl->cap[l];
-    }
-    ctl->qbase[NQ] = (int)min(acc, (long long)0x7fffffff);
-    if (acc > ws.qcap) ctl->error = ERR_CAPACITY;
+  // bucket regions: exclusive scan of the level capacities (waves 0-3)
+  __shared__ unsigned long long capq[4][NQ];
+  {  // sum the CAP_SLOTS partial histograms: 4 groups of 16 slots, then the groups
+    const int g = tid >> 8, lv = tid & (NQ - 1);
+    unsigned long long sum = 0;
+#pragma unroll
+    for (int k = 0; k < CAP_SLOTS / 4; ++k) sum += ws.capp[(g * (CAP_SLOTS / 4) + k) * NQ + lv];
+    capq[g][lv] = sum;
   }
-  const int per = (npxchunk + 1023) / 1024;
+  __syncthreads();
+  long long cv = 0, cx = 0;
+  if (tid < NQ) {
+    cv = (long long)(capq[0][tid] + capq[1][tid] + capq[2][tid] + capq[3][tid]);
+    cx = cv;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const long long y = __shfl_up(cx, o);
+      if ((tid & 63) >= o) cx += y;
+    }
+    if ((tid & 63) == 63) capw[tid >> 6] = cx;
+  }
+  const int per = ((npxchunk + 1023) / 1024 + 3) & ~3;
   const int a = min(npxchunk, tid * per), b = min(npxchunk, a + per);
   long long s = 0;
-  for (int c = a; c < b; ++c) s += ws.tot[c];
+  if (b - a == per) {
+    for (int c = a; c < b; c += 4) {
+      const int4 v = *reinterpret_cast<const int4*>(ws.tot + c);
+      s += (long long)v.x + v.y + v.z + v.w;
+    }
+  } else {
+    for (int c = a; c < b; ++c) s += ws.tot[c];
+  }
+  __syncthreads();
+  if (tid < NQ) {
+    long long base = cx - cv;
+    for (int k = 0; k < (tid >> 6); ++k) base += capw[k];
+    ctl->qbase[tid] = (int)base;
+    if (tid == NQ - 1) {
+      const long long acc = base + cv;
+      ctl->qbase[NQ] = (int)min(acc, (long long)0x7fffffff);
+      if (acc > ws.qcap) ctl->error = ERR_CAPACITY;
+    }
+  }
   const int lane = tid & 63, wv = tid >> 6;
   long long x = s;
   for (int o = 1; o < 64; o <<= 1) {
@@ -405,47 +525,41 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
   }
 }
 
-// Ordered compaction of the phase-1 pixels in raster order into ilist/desc + level histograms.
-// One block per raster chunk (an RSEG-column row segment); thread = 4 consecutive pixels of the
-// row, i.e. one tile row (32 B of its tile's line).
-__global__ __launch_bounds__(256) void k_compact(Ws ws) {
-  __shared__ int wt[4];
+// Ordered compaction of the phase-1 pixels in raster order into ilist/desc + level histograms:
+// one wave per raster chunk copies the chunk's list (k_prep's scratch in qbuf) to its offset.
+__device__ __forceinline__ int ld_state(const Ws& ws, long long t);
+
+__global__ __launch_bounds__(256) void k_compact(Ws ws, int nrc) {
   if (ws.ctl->bat.n == 0 || ws.ctl->bat.mode != 1) return;
-  const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-  const int r = blockIdx.x / ws.nseg, cs = blockIdx.x % ws.nseg;
-  const int c = cs * RSEG + tid * 4;
-  int lv[4] = {-1, -1, -1, -1};
-  int n = 0;
-  long long t0 = 0;
-  if (c < ws.W) {
-    t0 = tix(r, c, ws.Wt);
-    const int4 a = *reinterpret_cast<const int4*>(ws.mk + (t0 << 1));
-    const int4 b = *reinterpret_cast<const int4*>(ws.mk + (t0 << 1) + 4);
-    const int s[4] = {a.x, a.z, b.x, b.z};
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (c + k < ws.W && is_p1(s[k])) {
-        lv[k] = s[k] & 255;
-        ++n;
-      }
-  }
-  int x = n;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wt[wv] = x;
-  __syncthreads();
-  long long k = (long long)ws.choff[blockIdx.x] + (x - n);
-  for (int w = 0; w < wv; ++w) k += wt[w];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    if (lv[q] < 0) continue;
-    ws.ilist[k] = (int32_t)(t0 + q);
-    ws.desc[k] = make_desc((unsigned)lv[q], 1u, 0, 0);
-    atomicAdd(&ws.cnt[(k / CH) * NQ + lv[q]], 1);
-    ++k;
+  const int lane = lane_id();
+  const int ch = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ch >= nrc) return;
+  const int n = ws.tot[ch];
+  if (n == 0) return;
+  const int r = ch / ws.nseg, cs = ch % ws.nseg;
+  const long long rs = (long long)r * ws.W + (long long)cs * RSEG;
+  const long long k0 = ws.choff[ch];
+  for (int j0 = 0; j0 < n; j0 += 64) {  // wave-uniform
+    const int j = j0 + lane;
+    const bool on = j < n;
+    const long long k = k0 + j;
+    long long bin = -1;
+    if (on) {
+      const int t = ws.qbuf[rs + j];
+      const int lv = ld_state(ws, t) & 255;
+      ws.ilist[k] = t;
+      ws.desc[k] = make_desc((unsigned)lv, 1u, 0, 0);
+      bin = (k / CH) * NQ + lv;
+    }
+    // plateau seeds share a level: one atomic per distinct histogram bin of the wave
+    unsigned long long rem = __ballot(on);
+    while (rem) {
+      const int leader = __ffsll((long long)rem) - 1;
+      const long long lb = __shfl(bin, leader);
+      const unsigned long long same = __ballot(on && bin == lb);
+      if (lane == leader) atomicAdd(&ws.cnt[lb], (int)__popcll(same));
+      rem &= ~same;
+    }
   }
 }
 
@@ -460,82 +574,150 @@ __device__ __forceinline__ int fold_lab(int lab, int v) {
 }
 
 
-__device__ __forceinline__ unsigned long long claim_tag(unsigned epoch, int rank) {
-  return ((unsigned long long)epoch << 32) | (unsigned long long)(0xffffffffu - (unsigned)rank);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Large batches: labels in k_resolve, push decisions in k_claim.
-//
-// k_resolve: label of every item = fold of its settled neighbours and of the labels of EARLIER
-// batch items adjacent to it (the only intra-batch dependency left: rare, usually in-wave).
-// Ranks are dealt round-robin over the whole grid (block-round r covers ranks
-// [r*G*BS, (r+1)*G*BS)), so a lower rank is in the same round (a co-resident block: grid <=
-// RES_GRID_MAX) or an earlier one: bounded spinning cannot deadlock.  In-wave dependencies go
-// through register shuffles, others through 8-byte {epoch, label} granules.  A non-WSHED item then
-// CLAIMS each 0-neighbour with atomicMax({epoch, ~rank}): the surviving claim is the smallest rank
-// among the non-WSHED items adjacent to that pixel -- serially the first one to push it.
-struct LItem {
+struct Item {
   long long p;
-  int base_lab;
+  int base_lab;      // fold of the settled (>0) neighbours: 0, a label, or WSHED
   unsigned zero_mask;
-  unsigned wts;
-  int ldep[4];
+  unsigned wts;      // 4 packed 8-bit edge weights, directions L,R,T,B
+  int dep[16];       // 0..3 label deps, 4+3d+k push deps (earlier items adjacent to the d-target)
 };
 
-__device__ __forceinline__ void gather_label(const Ws& ws, const Seg* segs, int nseg, int i, int slot,
-                                             LItem& it) {
+__device__ __forceinline__ void gather_item(const Ws& ws, const Seg* segs, int nseg, int i, int slot,
+                                            Item& it) {
   const int Wt = ws.Wt;
   const long long p = ws.qbuf[slot];
   it.p = p;
   it.base_lab = 0;
   it.zero_mask = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) it.dep[k] = -1;
   it.wts = ld_w4(ws, p);
+  long long nb[4];
   int v[4];
 #pragma unroll
-  for (int d = 0; d < 4; ++d) v[d] = ld_state(ws, nb_of(p, d, Wt));
+  for (int d = 0; d < 4; ++d) {
+    nb[d] = nb_of(p, d, Wt);
+    v[d] = ld_state(ws, nb[d]);
+  }
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    it.ldep[d] = -1;
     if (v[d] > 0) {
       it.base_lab = fold_lab(it.base_lab, v[d]);
     } else if (v[d] <= -3) {
       const int r = rank_of_slot(segs, nseg, state_slot(v[d]));
-      if (r >= 0 && r < i) it.ldep[d] = r;
+      if (r >= 0 && r < i) it.dep[d] = r;
     } else if (v[d] == 0) {
       it.zero_mask |= 1u << d;
     }
   }
+  if (it.base_lab == WSHED) return;  // WSHED absorbs: no label or push dependency matters
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if (!((it.zero_mask >> d) & 1u)) continue;
+    const long long n = nb[d];
+    // n's neighbours other than p (p is n's opposite-direction neighbour), directions ascending
+    const int e0 = (d == 1) ? 1 : 0;
+    const int e1 = (d <= 1) ? 2 : 1;
+    const int e2 = (d == 2) ? 2 : 3;
+    const long long o[3] = {nb_of(n, e0, Wt), nb_of(n, e1, Wt), nb_of(n, e2, Wt)};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int vo = ld_state(ws, o[k]);
+      if (vo <= -3) {
+        const int r = rank_of_slot(segs, nseg, state_slot(vo));
+        if (r >= 0 && r < i) it.dep[4 + 3 * d + k] = r;
+      }
+    }
+  }
 }
 
+// Try to decide the item.  fetch(rank) -> resolved label of an earlier item, 0 = not yet.
+template <class F>
+__device__ __forceinline__ bool attempt_item(const Item& it, F fetch, int& lab_out, unsigned& mask_out) {
+  int lab = it.base_lab;
+  bool unknown = false;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int r = it.dep[d];
+    if (r >= 0) {
+      const int v = fetch(r);
+      if (v == 0) unknown = true;
+      else if (v > 0) lab = fold_lab(lab, v);
+    }
+  }
+  if (lab == WSHED) {
+    lab_out = WSHED;
+    mask_out = 0;
+    return true;
+  }
+  if (unknown) return false;
+  unsigned m = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if (!((it.zero_mask >> d) & 1u)) continue;
+    bool lose = false, undecided = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int r = it.dep[4 + 3 * d + k];
+      if (r >= 0) {
+        const int v = fetch(r);
+        if (v > 0) lose = true;
+        else if (v == 0) undecided = true;
+      }
+    }
+    if (!lose) {
+      if (undecided) return false;
+      m |= 1u << d;
+    }
+  }
+  lab_out = lab;
+  mask_out = m;
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Large batches: one kernel decides every item, k_scatter commits.
+//
+// k_resolve: label of an item = fold of its settled neighbours and of the labels of EARLIER batch
+// items adjacent to it; it pushes a 0-neighbour z unless an earlier batch item adjacent to z has
+// a non-WSHED label (serially that item pushed z first).  Both only wait on LOWER ranks.  Ranks
+// are dealt round-robin over the co-resident grid (block-round r covers ranks
+// [r*G*RBS, (r+1)*G*RBS)), so a lower rank is in the same round or an earlier one: bounded
+// spinning cannot deadlock.  In-wave dependencies go through register shuffles, others through
+// 8-byte granules {epoch, label} (final) or {epoch | bit 63, base fold} (provisional: a pending
+// dep whose settled neighbours fold to b can only end as b or WSHED).  Items then add their
+// pushes to the per-chunk level histograms and the cut words; the last block to finish (arrival
+// ticket) runs the scan, and when the committed batch is small also its scatter and the
+// small-batch loop.
+__device__ Batch scan_body(const Ws& ws);
+__device__ void scatter_chunks(const Ws& ws, const Batch& B, int first, int stride);
 __device__ __forceinline__ void small_loop(const Ws& ws);
 
-// Small batches reach this kernel only right after a large one (k_claim's last block runs the
-// small_loop once nothing is left for k_scatter).
 __global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
-  if (B.n == 0 || B.mode != 0 || ctl->error) return;
+  const bool work = !(B.n == 0 || B.mode != 0 || ctl->error);
   __shared__ Seg segs[NQ];
-  load_segs(ctl, B, segs);
-  __syncthreads();
+  __shared__ int hist[NQ];
+  __shared__ int s_minpush;
+  if (work) load_segs(ctl, B, segs);
+  if (threadIdx.x == 0) s_minpush = NQ;
   const int tid = threadIdx.x, lane = lane_id();
   const unsigned long long etag = (unsigned long long)B.epoch << 32;  // final label granule
   const unsigned long long ptag = etag | (1ull << 63);                // provisional base fold
-  const int Wt = ws.Wt;
   unsigned long long* const dg = ws.diag;
-  for (int base = blockIdx.x * RBS; base < B.n; base += gridDim.x * RBS) {
+  for (int base = blockIdx.x * RBS; work && base < B.n; base += gridDim.x * RBS) {
+    if (tid < NQ) hist[tid] = 0;
+    __syncthreads();
     const int wbase = base + (tid & ~63);
     const int i = wbase + lane;
     const bool valid = i < B.n;
     const unsigned long long t_a = dg ? __builtin_amdgcn_s_memtime() : 0;
-    long long iters = 0;
-    LItem it;
+    Item it;
     int sg = 0;
     if (valid) {
       sg = (B.nseg == 1) ? 0 : seg_of_rank(segs, B.nseg, i);
-      const int slot = segs[sg].bstart + (i - segs[sg].rank);
-      gather_label(ws, segs, B.nseg, i, slot, it);
+      gather_item(ws, segs, B.nseg, i, segs[sg].bstart + (i - segs[sg].rank), it);
       ws.ipx[i] = (int32_t)it.p;
     } else {
       it.p = 0;
@@ -543,41 +725,46 @@ __global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
       it.zero_mask = 0;
       it.wts = 0;
 #pragma unroll
-      for (int d = 0; d < 4; ++d) it.ldep[d] = -1;
+      for (int k = 0; k < 16; ++k) it.dep[k] = -1;
     }
-    unsigned inw_slots = 0;  // wave-uniform: which dependency slots point inside this wave
+    unsigned inw = 0;  // wave-uniform: dependency slots that point inside this wave
+    bool anydep = false;
 #pragma unroll
-    for (int d = 0; d < 4; ++d)
-      if (__any((unsigned)(it.ldep[d] - wbase) < 64u)) inw_slots |= 1u << d;
-    const bool any_dep = __any(it.ldep[0] >= 0 || it.ldep[1] >= 0 || it.ldep[2] >= 0 || it.ldep[3] >= 0);
-    bool pending = valid;
+    for (int k = 0; k < 16; ++k) {
+      if (__any((unsigned)(it.dep[k] - wbase) < 64u)) inw |= 1u << k;
+      anydep |= it.dep[k] >= 0;
+    }
+    anydep = __any(anydep);
+    bool lab_done = !valid, push_done = !valid, published = false;
     int mylab = 0;
-    long long t0 = 0;
+    long long t0 = 0, iters = 0;
     int spins = 0;
     const unsigned long long t_b = dg ? __builtin_amdgcn_s_memtime() : 0;
-    bool published = false;
     for (;;) {
-      int snap[4] = {0, 0, 0, 0}, sbase[4] = {0, 0, 0, 0};
-      if (any_dep) {
+      int snap[16], sbase[4];
 #pragma unroll
-        for (int d = 0; d < 4; ++d)
-          if ((inw_slots >> d) & 1u) {
-            const int r = it.ldep[d];
+      for (int k = 0; k < 16; ++k) snap[k] = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sbase[k] = 0;
+      if (anydep) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if ((inw >> k) & 1u) {
+            const int r = it.dep[k];
             const int src = ((unsigned)(r - wbase) < 64u) ? r - wbase : lane;
-            snap[d] = __shfl(mylab, src);
-            sbase[d] = __shfl(it.base_lab, src);
+            snap[k] = __shfl(mylab, src);
+            if (k < 4) sbase[k] = __shfl(it.base_lab, src);
           }
       }
-      if (pending) {
-        // fold the settled labels and the FINAL labels of resolved deps; a dep still pending whose
-        // base fold b (its settled neighbours) is WSHED or already in the fold is redundant: it
-        // ends as b or WSHED, and WSHED is not folded
+      if (!lab_done) {
+        // fold the settled labels and the final labels of resolved deps; a pending dep whose
+        // base fold is WSHED or already in the fold is redundant
         int lab = it.base_lab;
         int prov[4] = {0, 0, 0, 0};
         unsigned pm = 0;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
-          const int r = it.ldep[d];
+          const int r = it.dep[d];
           if (r < 0) continue;
           int v, pb;
           if ((unsigned)(r - wbase) < 64u) {
@@ -611,24 +798,74 @@ __global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
           }
           mylab = lab;
           st_granule(&ws.tl[i], etag | (uint32_t)lab);
-          const unsigned zm = (lab == WSHED) ? 0u : it.zero_mask;
-          ws.desc[i] = make_desc(it.wts, zm, segs[sg].L, sg);
-          const unsigned long long ct = claim_tag(B.epoch, i);
+          lab_done = true;
+        }
+      }
+      if (lab_done && !push_done) {
+        // push to 0-neighbour z unless an earlier batch item adjacent to z is non-WSHED
+        unsigned m = 0;
+        bool undecided = false;
+        if (mylab != WSHED) {
 #pragma unroll
-          for (int d = 0; d < 4; ++d)
-            if ((zm >> d) & 1u) atomicMax(&ws.claim[nb_of(it.p, d, Wt)], ct);
-          pending = false;
+          for (int d = 0; d < 4; ++d) {
+            if (!((it.zero_mask >> d) & 1u)) continue;
+            bool lose = false, und = false;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              const int r = it.dep[4 + 3 * d + k];
+              if (r < 0) continue;
+              int v;
+              if ((unsigned)(r - wbase) < 64u) {
+                v = snap[4 + 3 * d + k];
+              } else {
+                const unsigned long long g = ld_granule(&ws.tl[r]);
+                v = ((g & 0xffffffff00000000ull) == etag) ? (int)(uint32_t)g : 0;
+              }
+              if (v > 0) lose = true;
+              else if (v == 0) und = true;
+            }
+            if (!lose) {
+              if (und) undecided = true;
+              else m |= 1u << d;
+            }
+          }
+        }
+        if (!undecided) {
+          push_done = true;
+          const int lvi = segs[sg].L;
+          ws.desc[i] = make_desc(it.wts, m, lvi, sg);
+          bool lower = false;
+          int tmin = NQ;
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            if (!((m >> d) & 1u)) continue;
+            const int lv = (it.wts >> (8 * d)) & 255;
+            atomicAdd(&hist[lv], 1);
+            if (lv < lvi) lower = true;
+            else tmin = min(tmin, lv);
+          }
+          if (lower) {
+            atomicMin(&ctl->cut, i);
+            atomicMin(&s_minpush, 0);
+          }
+          if (tmin < NQ) {
+            atomicMin(&s_minpush, tmin);
+            if (B.nseg > 1) {
+              const int mc = seg_cut_for(segs, B.nseg, sg, tmin);
+              if (mc != NONE) atomicMin(&ctl->segcut, mc);
+            }
+          }
         }
       }
       ++iters;
-      if (!__any(pending)) break;
+      if (!__any(!push_done)) break;
       if (++spins > 16) {
         __builtin_amdgcn_s_sleep(1);
         if (__hip_atomic_load(&ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
         const long long now = (long long)__builtin_amdgcn_s_memrealtime();
         if (t0 == 0) t0 = now;
         else if (now - t0 > SPIN_LIMIT_TICKS) {
-          if (pending) atomicOr(&ctl->error, ERR_TIMEOUT);
+          if (!push_done) atomicOr(&ctl->error, ERR_TIMEOUT);
           break;
         }
       }
@@ -641,73 +878,10 @@ __global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
       atomicMax(&dg[3], t_c - t_b);
       atomicAdd(&dg[4], 1ull);
     }
-  }
-}
-
-// k_claim: push decisions from the surviving claims, per-chunk level histograms (one global
-// atomic per block-round and level), the interrupt cut (push below the item's own level: cut
-// after the item) and the segment cut (push below a LATER segment's level: end the batch before
-// that segment), and the lowest pushed level.  No waiting: every claim of the batch was made
-// before this kernel started.
-__device__ Batch scan_body(const Ws& ws);
-__device__ void scatter_chunks(const Ws& ws, const Batch& B, int first, int stride);
-
-// Claim check + per-chunk level histograms, 1024-thread blocks.  The last block to finish (atomic
-// ticket, agent-scope fences on both sides) runs the scan itself, saving a kernel boundary per
-// iteration; when there is nothing to claim (end of flood, error) the blocks only take the ticket.
-__global__ __launch_bounds__(1024) void k_claim(Ws ws) {
-  Ctl* ctl = ws.ctl;
-  const Batch B = ctl->bat;
-  const bool work = !(B.n == 0 || B.mode != 0 || ctl->error);
-  __shared__ int hist[NQ];
-  __shared__ Seg segs[NQ];
-  __shared__ int s_minpush;
-  if (work) load_segs(ctl, B, segs);
-  if (threadIdx.x == 0) s_minpush = NQ;
-  const int tid = threadIdx.x;
-  const int Wt = ws.Wt;
-  for (int base = blockIdx.x * 1024; work && base < B.n; base += gridDim.x * 1024) {
-    if (tid < NQ) hist[tid] = 0;
-    __syncthreads();
-    const int i = base + tid;
-    if (i < B.n) {
-      const unsigned long long d = ws.desc[i];
-      const unsigned zm = (unsigned)(d >> 32) & 15u;
-      if (zm) {
-        const unsigned wts = (unsigned)d;
-        const int lvi = (int)((d >> 40) & 255), sg = (int)((d >> 48) & 255);
-        const long long p = ws.ipx[i];
-        const unsigned long long ct = claim_tag(B.epoch, i);
-        unsigned push = 0;
-        bool lower = false;
-        int tmin = NQ;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (!((zm >> k) & 1u)) continue;
-          if (ws.claim[nb_of(p, k, Wt)] == ct) {
-            push |= 1u << k;
-            const int lv = (wts >> (8 * k)) & 255;
-            atomicAdd(&hist[lv], 1);
-            if (lv < lvi) lower = true;
-            else tmin = min(tmin, lv);
-          }
-        }
-        ws.desc[i] = (d & ~(15ull << 32)) | ((unsigned long long)push << 32);
-        if (lower) atomicMin(&ctl->cut, i);
-        if (tmin < NQ) {
-          atomicMin(&s_minpush, tmin);
-          if (B.nseg > 1) {
-            const int m = seg_cut_for(segs, B.nseg, sg, tmin);
-            if (m != NONE) atomicMin(&ctl->segcut, m);
-          }
-        }
-        if (lower) atomicMin(&s_minpush, 0);
-      }
-    }
     __syncthreads();
     if (tid < NQ && hist[tid]) atomicAdd(&ws.cnt[(long long)(base / CH) * NQ + tid], hist[tid]);
-    __syncthreads();
   }
+  __syncthreads();
   if (tid == 0 && s_minpush < NQ) atomicMin(&ctl->minpush, s_minpush);
   // arrival ticket (every path takes it: no block may read ctl->bat after the scan rewrote it).
   // Publish: drain every wave, barrier, ONE agent release fence, drain, relaxed ticket add.
@@ -974,107 +1148,6 @@ __global__ __launch_bounds__(1024) void k_scatter(Ws ws) {
 // push decisions are pulled directly (an earlier non-WSHED batch item adjacent to the target
 // pushes it first) instead of claimed.  Exits, writing the queue state back, when the next batch
 // is larger than SMALL_MAX, the flood is done, or on error.
-struct Item {
-  long long p;
-  int base_lab;      // fold of the settled (>0) neighbours: 0, a label, or WSHED
-  unsigned zero_mask;
-  unsigned wts;      // 4 packed 8-bit edge weights, directions L,R,T,B
-  int dep[16];       // 0..3 label deps, 4+3d+k push deps (earlier items adjacent to the d-target)
-};
-
-__device__ __forceinline__ void gather_item(const Ws& ws, const Seg* segs, int nseg, int i, int slot,
-                                            Item& it) {
-  const int Wt = ws.Wt;
-  const long long p = ws.qbuf[slot];
-  it.p = p;
-  it.base_lab = 0;
-  it.zero_mask = 0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) it.dep[k] = -1;
-  it.wts = ld_w4(ws, p);
-  long long nb[4];
-  int v[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    nb[d] = nb_of(p, d, Wt);
-    v[d] = ld_state(ws, nb[d]);
-  }
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    if (v[d] > 0) {
-      it.base_lab = fold_lab(it.base_lab, v[d]);
-    } else if (v[d] <= -3) {
-      const int r = rank_of_slot(segs, nseg, state_slot(v[d]));
-      if (r >= 0 && r < i) it.dep[d] = r;
-    } else if (v[d] == 0) {
-      it.zero_mask |= 1u << d;
-    }
-  }
-  if (it.base_lab == WSHED) return;  // WSHED absorbs: no label or push dependency matters
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    if (!((it.zero_mask >> d) & 1u)) continue;
-    const long long n = nb[d];
-    // n's neighbours other than p (p is n's opposite-direction neighbour), directions ascending
-    const int e0 = (d == 1) ? 1 : 0;
-    const int e1 = (d <= 1) ? 2 : 1;
-    const int e2 = (d == 2) ? 2 : 3;
-    const long long o[3] = {nb_of(n, e0, Wt), nb_of(n, e1, Wt), nb_of(n, e2, Wt)};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int vo = ld_state(ws, o[k]);
-      if (vo <= -3) {
-        const int r = rank_of_slot(segs, nseg, state_slot(vo));
-        if (r >= 0 && r < i) it.dep[4 + 3 * d + k] = r;
-      }
-    }
-  }
-}
-
-// Try to decide the item.  fetch(rank) -> resolved label of an earlier item, 0 = not yet.
-template <class F>
-__device__ __forceinline__ bool attempt_item(const Item& it, F fetch, int& lab_out, unsigned& mask_out) {
-  int lab = it.base_lab;
-  bool unknown = false;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const int r = it.dep[d];
-    if (r >= 0) {
-      const int v = fetch(r);
-      if (v == 0) unknown = true;
-      else if (v > 0) lab = fold_lab(lab, v);
-    }
-  }
-  if (lab == WSHED) {
-    lab_out = WSHED;
-    mask_out = 0;
-    return true;
-  }
-  if (unknown) return false;
-  unsigned m = 0;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    if (!((it.zero_mask >> d) & 1u)) continue;
-    bool lose = false, undecided = false;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int r = it.dep[4 + 3 * d + k];
-      if (r >= 0) {
-        const int v = fetch(r);
-        if (v > 0) lose = true;
-        else if (v == 0) undecided = true;
-      }
-    }
-    if (!lose) {
-      if (undecided) return false;
-      m |= 1u << d;
-    }
-  }
-  lab_out = lab;
-  mask_out = m;
-  return true;
-}
-
 __device__ __forceinline__ void small_loop(const Ws& ws) {
   constexpr int NW = 16;
   Ctl* ctl = ws.ctl;
@@ -1376,6 +1449,8 @@ __global__ __launch_bounds__(256) void k_untile(const int32_t* __restrict__ mk, 
                                                 int32_t* __restrict__ lab, int depth,
                                                 const uint8_t* __restrict__ pal,
                                                 uint8_t* __restrict__ dst, uint8_t* __restrict__ gray) {
+  // lane = one 16-B unit {state, w4, state, w4} = 2 pixels of a tile row: loads are lane-
+  // contiguous, and the 16 lanes of one tile row of 8 consecutive tiles store 128 B of labels
   extern __shared__ __attribute__((aligned(16))) uint32_t spal[];
   const bool lds_pal = dst != nullptr && pal != nullptr && depth <= PAL_LDS_MAX;
   if (lds_pal) {
@@ -1383,53 +1458,49 @@ __global__ __launch_bounds__(256) void k_untile(const int32_t* __restrict__ mk, 
       spal[k] = (uint32_t)pal[3 * k] | ((uint32_t)pal[3 * k + 1] << 8) | ((uint32_t)pal[3 * k + 2] << 16);
     __syncthreads();
   }
-  const long long ntiles = (long long)((H + 3) >> 2) * Wt;
-  const bool vec = (W & 3) == 0 && (((uintptr_t)lab) & 15) == 0;
-  const bool vec3 = (W & 3) == 0 && dst != nullptr && (((uintptr_t)dst) & 3) == 0;
-  const bool vecg = (W & 3) == 0 && gray != nullptr && (((uintptr_t)gray) & 3) == 0;
-  for (long long tt = (long long)blockIdx.x * blockDim.x + threadIdx.x; tt < ntiles;
-       tt += (long long)gridDim.x * blockDim.x) {
-    const int r0 = (int)(tt / Wt) * 4, c0 = (int)(tt % Wt) * 4;
-    const int4* src = reinterpret_cast<const int4*>(mk + (tt << 5));
-#pragma unroll
-    for (int ry = 0; ry < 4; ++ry) {
-      const int r = r0 + ry;
-      if (r >= H) break;
-      const int4 a = src[2 * ry], b = src[2 * ry + 1];
-      const int l[4] = {a.x, a.z, b.x, b.z};
-      const long long q = (long long)r * W + c0;
-      const bool full = c0 + 4 <= W;
-      if (full && vec) {
-        *reinterpret_cast<int4*>(lab + q) = make_int4(l[0], l[1], l[2], l[3]);
-      } else {
-        for (int k = 0; k < 4 && c0 + k < W; ++k) lab[q + k] = l[k];
+  const long long nunits = (long long)((H + 3) >> 2) * Wt * 8;
+  const bool even = (W & 1) == 0;
+  const bool v2 = even && (((uintptr_t)lab) & 7) == 0;
+  const bool v3 = even && dst != nullptr && (((uintptr_t)dst) & 1) == 0;
+  const bool vg = even && gray != nullptr && (((uintptr_t)gray) & 1) == 0;
+  for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < nunits;
+       u += (long long)gridDim.x * blockDim.x) {
+    const long long tt = u >> 3;
+    const int k = (int)(u & 7);
+    const int r = (int)(tt / Wt) * 4 + (k >> 1), c = (int)(tt % Wt) * 4 + 2 * (k & 1);
+    if (r >= H || c >= W) continue;
+    const int4 a = reinterpret_cast<const int4*>(mk)[u];
+    const int l[2] = {a.x, a.z};
+    const long long q = (long long)r * W + c;
+    const bool both = c + 1 < W;
+    if (both && v2) *reinterpret_cast<int2*>(lab + q) = make_int2(l[0], l[1]);
+    else for (int j = 0; j < 2 && c + j < W; ++j) lab[q + j] = l[j];
+    if (dst == nullptr) continue;
+    const uint32_t c0 = label_colour(l[0], depth, pal, lds_pal, spal);
+    const uint32_t c1 = label_colour(l[1], depth, pal, lds_pal, spal);
+    uint8_t* o = dst + q * 3;
+    if (both && v3) {  // B0G0 R0B1 G1R1
+      reinterpret_cast<uint16_t*>(o)[0] = (uint16_t)(c0 & 0xffffu);
+      reinterpret_cast<uint16_t*>(o)[1] = (uint16_t)(((c0 >> 16) & 0xffu) | ((c1 & 0xffu) << 8));
+      reinterpret_cast<uint16_t*>(o)[2] = (uint16_t)((c1 >> 8) & 0xffffu);
+    } else {
+      const uint32_t cc[2] = {c0, c1};
+      for (int j = 0; j < 2 && c + j < W; ++j) {
+        o[3 * j] = cc[j] & 255;
+        o[3 * j + 1] = (cc[j] >> 8) & 255;
+        o[3 * j + 2] = (cc[j] >> 16) & 255;
       }
-      if (dst == nullptr) continue;
-      uint32_t col[4];
+    }
+    if (gray) {
+      const uint32_t cc[2] = {c0, c1};
+      uint32_t g2 = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) col[k] = label_colour(l[k], depth, pal, lds_pal, spal);
-      uint8_t* o = dst + q * 3;
-      if (full && vec3) {  // 12 bytes: B0G0R0B1 G1R1B2G2 R2B3G3R3
-        reinterpret_cast<uint32_t*>(o)[0] = (col[0] & 0xffffffu) | (col[1] << 24);
-        reinterpret_cast<uint32_t*>(o)[1] = ((col[1] >> 8) & 0xffffu) | (col[2] << 16);
-        reinterpret_cast<uint32_t*>(o)[2] = ((col[2] >> 16) & 0xffu) | (col[3] << 8);
-      } else {
-        for (int k = 0; k < 4 && c0 + k < W; ++k) {
-          o[3 * k] = col[k] & 255;
-          o[3 * k + 1] = (col[k] >> 8) & 255;
-          o[3 * k + 2] = (col[k] >> 16) & 255;
-        }
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t bb = cc[j] & 255, gg = (cc[j] >> 8) & 255, rr = (cc[j] >> 16) & 255;
+        g2 |= ((1868u * bb + 9617u * gg + 4899u * rr + 8192u) >> 14) << (8 * j);
       }
-      if (gray) {
-        uint32_t g4 = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t bb = col[k] & 255, gg = (col[k] >> 8) & 255, rr = (col[k] >> 16) & 255;
-          g4 |= ((1868u * bb + 9617u * gg + 4899u * rr + 8192u) >> 14) << (8 * k);
-        }
-        if (full && vecg) *reinterpret_cast<uint32_t*>(gray + q) = g4;
-        else for (int k = 0; k < 4 && c0 + k < W; ++k) gray[q + k] = (g4 >> (8 * k)) & 255;
-      }
+      if (both && vg) *reinterpret_cast<uint16_t*>(gray + q) = (uint16_t)g2;
+      else for (int j = 0; j < 2 && c + j < W; ++j) gray[q + j] = (g2 >> (8 * j)) & 255;
     }
   }
 }

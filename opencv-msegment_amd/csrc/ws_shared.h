@@ -25,6 +25,7 @@ constexpr long long SPIN_LIMIT_TICKS = 200000000ll;  // 2 s of s_memrealtime (10
 // Per-pixel flood state is TILED: 4x4-pixel tiles of 8-byte {state, w4} words (128 B = one L2
 // line per tile), tiles row-major, Wt tiles per tile row.  A pixel and its 4 neighbours mostly
 // share a line, so a queue item costs ~2 random lines instead of ~4.
+constexpr int CAP_SLOTS = 64;  // spread of the capacity-histogram atomics (same-address contention)
 constexpr int RSEG = 1024;  // columns per raster chunk of the phase-1 compaction (256 tiles)
 __host__ __device__ inline long long tix(int r, int c, int Wt) {
   return ((long long)((long long)(r >> 2) * Wt + (c >> 2)) << 4) | ((r & 3) << 2) | (c & 3);
@@ -77,14 +78,13 @@ struct Ctl {
   int qbase[NQ + 1];
   int qhead[NQ];
   int qtail[NQ];
-  unsigned cap[NQ];
   Batch bat;    // current batch (written by k_init_scan / k_scan / k_small)
   Batch cbat;   // batch being committed by k_scatter (written by k_scan)
   Seg seg[NQ];  // segments of the current batch
   int cut;      // first rank of the current batch that pushes below its own level (NONE: none)
   int segcut;   // first segment invalidated by a push below its level (NONE: none)
   int minpush;  // lowest level pushed by the current batch (merge heuristic)
-  unsigned ticket;  // k_claim blocks finished this iteration (the last one runs the scan)
+  unsigned ticket;  // k_resolve blocks finished this iteration (the last one runs the scan)
   int done;
   int error;
   int remaining;  // queued items after the last batch was formed (host polling hint)
@@ -101,12 +101,12 @@ struct Ws {
   int32_t* ilist;
   unsigned long long* tl;
   unsigned long long* desc;
-  unsigned long long* claim;  // per tiled pixel {epoch, ~rank} push claims (k_resolve -> k_claim)
-  int32_t* ipx;      // pixel of each rank of the current batch (k_resolve -> k_claim, k_scatter)
+  int32_t* ipx;      // pixel of each rank of the current batch (k_resolve -> k_scatter)
   int32_t* cnt;
   int32_t* coff;
   int32_t* tot;      // phase-1 pixels per raster chunk (k_prep -> k_init_scan)
   int32_t* choff;
+  unsigned* capp;    // CAP_SLOTS x NQ partial bucket-capacity histograms (k_prep -> k_init_scan)
   Ctl* ctl;
   unsigned long long* diag;  // nullptr = off; else 8 counters (msg_set_diag)
   int H, W;
