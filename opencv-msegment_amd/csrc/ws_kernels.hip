@@ -333,7 +333,8 @@ __device__ int block_sum(int v) {  // every thread of the block calls; result to
 // above that lowest level: a batch that did not feed its own or a lower level is unlikely to
 // start a generation, so later segments are unlikely to be cut (the cut rules keep it exact).
 __device__ void form_batch(const int* qbase, const int* head, const int* tail, int minpush,
-                           Seg* segs, int* nseg_out, int* n_out) {
+                           int wcap, Seg* segs, int* nseg_out, int* n_out) {
+  const int capn = (wcap > 0 && wcap < MERGE_CAP) ? wcap : MERGE_CAP;
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
   int cnt[4];
@@ -365,16 +366,16 @@ __device__ void form_batch(const int* qbase, const int* head, const int* tail, i
   for (int k = 0; k < 4; ++k) {
     if (cnt[k] <= 0) continue;
     const int l = lane * 4 + k;
-    const bool inc = (segi == 0) || (merge && cum + cnt[k] <= MERGE_CAP);
+    const bool inc = (segi == 0) || (merge && cum + cnt[k] <= capn);
     if (inc) {
       Seg s;
       s.L = l;
       s.bstart = qbase[l] + head[l];
       s.rank = cum;
-      s.n = cnt[k];
+      s.n = (segi == 0) ? min(cnt[k], capn) : cnt[k];  // the window truncates the first segment
       segs[segi] = s;
       ++inc_n;
-      inc_items += cnt[k];
+      inc_items += s.n;
     }
     cum += cnt[k];
     ++segi;
@@ -989,7 +990,9 @@ __device__ Batch scan_body(const Ws& ws) {
   }
   // the histogram rows this batch accumulated are zeroed by k_scatter (cbat.n covers them all)
   __syncthreads();
-  form_batch(s_base, s_head, s_tail, B.mode == 0 ? minpush : 0, nsegs, &s_nseg, &s_n);
+  const int wcap = (B.mode == 0) ? next_wcap(ctl->wcap, B.n, ncommit, cut != NONE && ncommit == cut + 1)
+                                 : ctl->wcap;
+  form_batch(s_base, s_head, s_tail, B.mode == 0 ? minpush : 0, wcap, nsegs, &s_nseg, &s_n);
   __syncthreads();
   const int ns = s_nseg;
   for (int k = tid; k < ns; k += blockDim.x) ctl->seg[k] = nsegs[k];
@@ -1008,6 +1011,7 @@ __device__ Batch scan_body(const Ws& ws) {
     nb.L = (ns > 0) ? nsegs[0].L : -1;
     nb.bstart = (ns > 0) ? nsegs[0].bstart : 0;
     ctl->bat = nb;
+    ctl->wcap = wcap;
     ctl->cut = NONE;
     ctl->segcut = NONE;
     ctl->minpush = NQ;
@@ -1156,13 +1160,14 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
   __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ], s_tot[NQ];
   __shared__ int s_wcnt[NW][NQ];
   __shared__ Seg s_seg[NQ];
-  __shared__ int s_cut, s_segcut, s_minpush, s_err, s_nseg, s_n;
+  __shared__ int s_cut, s_segcut, s_minpush, s_err, s_nseg, s_n, s_wcap;
   __shared__ Batch s_B;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const int Wt = ws.Wt;
   if (tid == 0) {
     s_B = ctl->bat;
     s_err = ctl->error;
+    s_wcap = ctl->wcap;
   }
   if (tid < NQ) {
     s_qbase[tid] = ctl->qbase[tid];
@@ -1315,9 +1320,10 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
       nb_pops += ncommit;
       nb_items += B.n;
       nb_push += npush;
+      s_wcap = next_wcap(s_wcap, B.n, ncommit, s_cut != NONE && ncommit == s_cut + 1);
     }
     __syncthreads();
-    form_batch(s_qbase, s_head, s_tail, s_minpush, s_seg, &s_nseg, &s_n);
+    form_batch(s_qbase, s_head, s_tail, s_minpush, s_wcap, s_seg, &s_nseg, &s_n);
     __syncthreads();
     if (tid == 0) {
       Batch nb;
@@ -1351,6 +1357,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
   for (int k = tid; k < s_B.nseg; k += 1024) ctl->seg[k] = s_seg[k];
   if (tid == 0) {
     ctl->bat = s_B;
+    ctl->wcap = s_wcap;
     ctl->cut = NONE;
     ctl->segcut = NONE;
     ctl->minpush = NQ;

@@ -20,6 +20,16 @@ constexpr int RBS = 1024;          // threads per k_resolve block (also the smal
 constexpr int SMALL_MAX = 4096;    // batches up to this size run inside the one-workgroup k_small
 constexpr int PAL_LDS_MAX = 16384; // palettes up to this many labels are staged in LDS
 constexpr int MERGE_CAP = 1 << 22; // largest multi-segment batch (items)
+constexpr int WMIN = 1024;         // smallest batch window (one small-loop round)
+// Batch window after committing ncommit of n items: an interrupt cut (a push below the item's
+// level) means the queue order is turning over fast, so the next batch is a short prefix; a
+// batch that filled its window uncut quadruples it.  Prefixes of the queue order: exact.
+__host__ __device__ inline int next_wcap(int wcap, int n, int ncommit, bool icut) {
+  const int cap = wcap ? wcap : MERGE_CAP;
+  if (icut) return ncommit * 2 > WMIN ? ncommit * 2 : WMIN;
+  if (n >= cap) return (cap >= MERGE_CAP / 4) ? 0 : cap * 4;
+  return wcap;
+}
 constexpr long long SPIN_LIMIT_TICKS = 200000000ll;  // 2 s of s_memrealtime (100 MHz)
 
 // Per-pixel flood state is TILED: 4x4-pixel tiles of 8-byte {state, w4} words (128 B = one L2
@@ -85,6 +95,7 @@ struct Ctl {
   int segcut;   // first segment invalidated by a push below its level (NONE: none)
   int minpush;  // lowest level pushed by the current batch (merge heuristic)
   unsigned ticket;  // k_resolve blocks finished this iteration (the last one runs the scan)
+  int wcap;         // batch window (0 = whole buckets): shrinks after interrupt cuts, regrows
   int done;
   int error;
   int remaining;  // queued items after the last batch was formed (host polling hint)
