@@ -30,8 +30,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 
 # Algorithmic bytes (DESIGN.md "Kernels"): what each kernel must move at minimum per unit.
 BYTES_PER_PIXEL = {"k_prep": 15.0, "k_untile": 15.0, "k_colorize": 7.0, "k_edge_weights": 5.0}
-BYTES_PER_ITEM = {"k_resolve": 40.0}        # per batch item resolved
-BYTES_SCATTER = (24.0, 12.0)                # per committed item, per appended push
+# k_resolve per item: queue entry 4 + own weights 4 + 4 neighbour states 16, out ipx 4 + granule 8
+# + desc 8 (push-competitor reads are data dependent and not counted)
+BYTES_PER_ITEM = {"k_resolve": 44.0}        # per batch item resolved
+BYTES_SCATTER = (24.0, 8.0)                 # per committed item, per appended push
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")  # scripts/pmc_summary.py output
 E2E_BYTES_PER_PIXEL = 14.0                  # 3 B BGR + 4 B markers in, 4 B labels + 3 B BGR out
 
 
@@ -211,10 +214,17 @@ def main(argv=None):
         roof = None
         if kern:
             top = kern[0]
+            traffic, tsrc = None, None
+            if os.path.exists(PMC_SUMMARY):  # HBM bytes per launch from the committed PMC passes
+                pm = json.load(open(PMC_SUMMARY))
+                kk = pm.get("kernels", {}).get(top["kernel"])
+                if kk:
+                    traffic = round(kk["hbm_bytes_per_launch"])
+                    tsrc = "profiles/pmc_latest.json (%s; %s)" % (pm.get("correction"), pm.get("note", ""))
             roof = {"bound": "hbm", "kernel": top["kernel"], "achieved": top["achieved_gbs"],
                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(top["achieved_gbs"] / HBM_PEAK_GBS, 5) if top["achieved_gbs"] else None,
-                    "traffic": None,
+                    "traffic": traffic, "traffic_source": tsrc,
                     "alg_bytes_per_launch": top["alg_bytes_per_launch"], "avg_launch_us": top["avg_us"]}
         e2e_gbs = value * 1e6 * E2E_BYTES_PER_PIXEL / 1e9
         out = {

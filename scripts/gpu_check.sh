@@ -23,4 +23,8 @@ run bench 600 python bench.py "$@"
 [ -n "${EXTRA_BENCH:-}" ] && run bench_extra 600 python bench.py $EXTRA_BENCH
 run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass
 find "$OUT/prof" -name '*stats*' -exec cp {} "$OUT/" \; 2>/dev/null
+# HBM traffic: one counter group per rocprofv3 run, kernel trace only (MI355X_MICROARCH.md)
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  run pmc_$ctr 600 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_$ctr" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass
+done
 echo "== done"

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Fold rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs (separate passes) into per-kernel HBM bytes
+per launch.  FETCH_SIZE is doubled: on gfx950 it reports half the bytes of wide coalesced reads
+(MI355X_MICROARCH.md, HBM/rocprofv3 section; checked here on k_untile, whose 16-B-per-lane loads
+move a known 8 B per pixel).  Other read widths (random 4-8 B gathers) are uncalibrated.
+
+  python scripts/pmc_summary.py <dir with pmc_FETCH_SIZE/ and pmc_WRITE_SIZE/> <out.json> [note]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def load(path, counter):
+    tot = collections.defaultdict(float)
+    n = collections.Counter()
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            k = r["Kernel_Name"].split("(")[0].replace("msg::", "")
+            tot[k] += float(r["Counter_Value"])
+            n[k] += 1
+    return {k: (tot[k], n[k]) for k in tot}
+
+
+def main():
+    src, out = sys.argv[1], sys.argv[2]
+    fetch = load(os.path.join(src, "pmc_FETCH_SIZE"), "FETCH_SIZE")
+    write = load(os.path.join(src, "pmc_WRITE_SIZE"), "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(fetch) | set(write)):
+        fk, fn = fetch.get(k, (0.0, 1))
+        wk, wn = write.get(k, (0.0, 1))
+        res[k] = {"launches": max(fn, wn),
+                  "fetch_bytes_per_launch": 2.0 * 1024.0 * fk / max(fn, 1),
+                  "write_bytes_per_launch": 1024.0 * wk / max(wn, 1)}
+        res[k]["hbm_bytes_per_launch"] = res[k]["fetch_bytes_per_launch"] + res[k]["write_bytes_per_launch"]
+    doc = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs) of "
+                     "`python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass`",
+           "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes", "note": sys.argv[3] if len(sys.argv) > 3 else "",
+           "kernels": res}
+    json.dump(doc, open(out, "w"), indent=1)
+    for k, v in res.items():
+        print("%-12s launches %6d  fetch %10.0f  write %10.0f  B/launch" % (k, v["launches"], v["fetch_bytes_per_launch"], v["write_bytes_per_launch"]))
+
+
+if __name__ == "__main__":
+    main()
