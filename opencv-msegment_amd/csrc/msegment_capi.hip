@@ -250,7 +250,8 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   long long syncs = 0;
   for (;;) {
     for (int g = 0; g < c->group; ++g, ++it) {
-      LAUNCH(c, KID_RESOLVE, st, k_resolve, dim3(gres), dim3(RBS), 0, ws);  // + scan (last block)
+      LAUNCH(c, KID_RESOLVE, st, k_resolve, dim3(gres), dim3(RBS), 0, ws);
+      LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);  // + small batches
       LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws);
     }
     HIPCHK(c, hipGetLastError());
@@ -358,8 +359,8 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
       return MSG_EHIP;
     }
     // blocks of a k_resolve round wait on each other, so the grid must be co-resident: the
-    // occupancy answer (2 x 1024 threads per CU at k_resolve's 48 VGPRs), capped at 2
-    c->res_grid = cus * std::max(1, std::min(per, 2));
+    // occupancy answer (3 x 512 threads per CU at k_resolve's 80 VGPRs), capped at 4
+    c->res_grid = cus * std::max(1, std::min(per, 4));
   }
   *out = c;
   return MSG_OK;

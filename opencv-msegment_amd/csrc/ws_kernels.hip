@@ -576,7 +576,7 @@ __device__ __forceinline__ int fold_lab(int lab, int v) {
 
 
 struct Item {
-  long long p;
+  int p;             // tiled pixel index (frames <= 2^28 pixels)
   int base_lab;      // fold of the settled (>0) neighbours: 0, a label, or WSHED
   unsigned zero_mask;
   unsigned wts;      // 4 packed 8-bit edge weights, directions L,R,T,B
@@ -586,7 +586,7 @@ struct Item {
 __device__ __forceinline__ void gather_item(const Ws& ws, const Seg* segs, int nseg, int i, int slot,
                                             Item& it) {
   const int Wt = ws.Wt;
-  const long long p = ws.qbuf[slot];
+  const int p = ws.qbuf[slot];
   it.p = p;
   it.base_lab = 0;
   it.zero_mask = 0;
@@ -694,7 +694,7 @@ __device__ Batch scan_body(const Ws& ws);
 __device__ void scatter_chunks(const Ws& ws, const Batch& B, int first, int stride);
 __device__ __forceinline__ void small_loop(const Ws& ws);
 
-__global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
+__global__ __launch_bounds__(RBS, 6) void k_resolve(Ws ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
   const bool work = !(B.n == 0 || B.mode != 0 || ctl->error);
@@ -742,19 +742,16 @@ __global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
     int spins = 0;
     const unsigned long long t_b = dg ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
-      int snap[16], sbase[4];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) snap[k] = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) sbase[k] = 0;
+      // label phase: in-wave snapshots of the 4 label deps (label + base fold)
+      int snap[4] = {0, 0, 0, 0}, sbase[4] = {0, 0, 0, 0};
       if (anydep) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
+        for (int k = 0; k < 4; ++k)
           if ((inw >> k) & 1u) {
             const int r = it.dep[k];
             const int src = ((unsigned)(r - wbase) < 64u) ? r - wbase : lane;
             snap[k] = __shfl(mylab, src);
-            if (k < 4) sbase[k] = __shfl(it.base_lab, src);
+            sbase[k] = __shfl(it.base_lab, src);
           }
       }
       if (!lab_done) {
@@ -802,6 +799,18 @@ __global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
           lab_done = true;
         }
       }
+      // push phase: in-wave snapshots of the 12 push-competitor labels (after this round's labels)
+      int psnap[12];
+#pragma unroll
+      for (int k = 0; k < 12; ++k) psnap[k] = 0;
+      if (anydep) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k)
+          if ((inw >> (4 + k)) & 1u) {
+            const int r = it.dep[4 + k];
+            psnap[k] = __shfl(mylab, ((unsigned)(r - wbase) < 64u) ? r - wbase : lane);
+          }
+      }
       if (lab_done && !push_done) {
         // push to 0-neighbour z unless an earlier batch item adjacent to z is non-WSHED
         unsigned m = 0;
@@ -817,7 +826,7 @@ __global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
               if (r < 0) continue;
               int v;
               if ((unsigned)(r - wbase) < 64u) {
-                v = snap[4 + 3 * d + k];
+                v = psnap[3 * d + k];
               } else {
                 const unsigned long long g = ld_granule(&ws.tl[r]);
                 v = ((g & 0xffffffff00000000ull) == etag) ? (int)(uint32_t)g : 0;
@@ -884,30 +893,18 @@ __global__ __launch_bounds__(RBS) void k_resolve(Ws ws) {
   }
   __syncthreads();
   if (tid == 0 && s_minpush < NQ) atomicMin(&ctl->minpush, s_minpush);
-  // arrival ticket (every path takes it: no block may read ctl->bat after the scan rewrote it).
-  // Publish: drain every wave, barrier, ONE agent release fence, drain, relaxed ticket add.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(&ctl->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    hist[0] = (t == gridDim.x - 1);
-    if (t == gridDim.x - 1) {  // last arriver: acquire before reading the other blocks' output
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      ctl->ticket = 0;
-    }
-  }
-  __syncthreads();
-  if (!hist[0]) return;
+}
+
+// Scan (1 block x 1024) of the batch k_resolve decided; a committed batch of at most SMALL_MAX
+// items is scattered here too, and then, with nothing left for k_scatter, this block runs the
+// following small batches itself (small_loop).
+__global__ __launch_bounds__(1024) void k_scan(Ws ws) {
+  Ctl* ctl = ws.ctl;
   const Batch cb = scan_body(ws);
-  // a committed batch of at most SMALL_MAX items is scattered here; then, with nothing left for
-  // k_scatter, this block runs the following small batches itself (small_loop)
   if (cb.nchunk > 0 && cb.n <= SMALL_MAX && !ctl->error) {
     scatter_chunks(ws, cb, 0, 1);
     __syncthreads();
-    if (tid == 0) ctl->cbat.nchunk = 0;
+    if (threadIdx.x == 0) ctl->cbat.nchunk = 0;
   } else if (cb.nchunk > 0) {
     return;  // k_scatter commits it
   }
@@ -1022,8 +1019,6 @@ __device__ Batch scan_body(const Ws& ws) {
   if (tid == 0) ctl->remaining = q;
   return s_cb;  // block_sum's barriers made s_cb visible
 }
-
-__global__ __launch_bounds__(1024) void k_scan(Ws ws) { scan_body(ws); }
 
 // Stable rank of this lane's pushes among the wave's pushes of the same level, in (lane, dir)
 // order.  Writes the per-level wave totals to wrow[level].  Wave-uniform loop over the distinct
