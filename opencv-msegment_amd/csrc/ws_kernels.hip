@@ -88,87 +88,88 @@ __device__ __forceinline__ int cdiffp(uint32_t a, uint32_t b) {  // L-inf BGR di
   return max(max(d0, d1), d2);
 }
 
-constexpr int PREP_COLS = RSEG + 2;                 // strip columns incl. the 1-pixel halo
-constexpr int PREP_RAW = (3 * PREP_COLS + 8) / 4 + 1; // dwords of one BGR row segment
+constexpr int PREP_COLS = RSEG + 2;                  // strip columns incl. the 1-pixel halo
+constexpr int PREP_LDW = RSEG + 5;                   // LDS row stride (words): conflict-free stencil
+constexpr int PREP_RAW = (3 * PREP_COLS + 8) / 4 + 1;  // dwords of one BGR row segment
 
-__global__ __launch_bounds__(256) void k_prep(Ws ws, const int32_t* __restrict__ mk_in) {
-  static_assert(NQ == 256 && RSEG == 1024, "one thread per level and per tile of the strip");
+// thread = one tile row (4 pixels): tile tid >> 2, row tid & 3, so 4 consecutive lanes write one
+// whole 128-B tile line; frames are <= 2^28 pixels, so 32-bit offsets (3N < 2^30) suffice.
+__global__ __launch_bounds__(1024) void k_prep(Ws ws, const int32_t* __restrict__ mk_in) {
+  static_assert(NQ == 256 && RSEG == 1024, "strip = 256 tiles x 4 rows = 1024 threads");
   __shared__ unsigned caph[NQ];
   __shared__ uint32_t s_raw[6][PREP_RAW];
-  __shared__ uint32_t s_px[6][PREP_COLS];
-  __shared__ int32_t s_m[6][PREP_COLS];
-  __shared__ unsigned long long s_wsum[4];
+  __shared__ uint32_t s_px[6][PREP_LDW];
+  __shared__ int32_t s_m[6][PREP_LDW];
+  __shared__ unsigned long long s_wsum[16];
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const int H = ws.H, W = ws.W, Wt = ws.Wt;
   const int tr = blockIdx.x / ws.nseg, cs = blockIdx.x % ws.nseg;
   const int r0 = tr * 4, x0 = cs * RSEG;
   const int ncol = min(RSEG, W - x0) + 2;  // strip column j <-> image column x0 - 1 + j
-  const long long nbytes = 3ll * H * W;
-  caph[tid] = 0;
-  // ---- stage rows r0-1..r0+4 of the strip: markers as ints, BGR as aligned dwords; every load
-  // is issued into registers before the first LDS store (54 independent loads in flight) ----
+  const int nbytes = 3 * H * W;
+  if (tid < NQ) caph[tid] = 0;
+  // ---- stage rows r0-1..r0+4: all loads issued before the first LDS store ----
   const bool aligned = (((uintptr_t)ws.img) & 3) == 0;
-  long long a0[6];
-  int mreg[6][5];
-  uint32_t ireg[6][4];
+  int a0[6];
+  int mreg[6][2];
+  uint32_t ireg[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const int r = r0 - 1 + i;
     const bool rin = r >= 0 && r < H;
 #pragma unroll
-    for (int it = 0; it < 5; ++it) {
-      const int j = tid + 256 * it, c = x0 - 1 + j;
-      mreg[i][it] = (rin && j < ncol && c >= 0 && c < W) ? mk_in[(long long)r * W + c] : 0;
+    for (int it = 0; it < 2; ++it) {
+      const int j = tid + 1024 * it, c = x0 - 1 + j;
+      mreg[i][it] = (rin && j < ncol && c >= 0 && c < W) ? mk_in[r * W + c] : 0;
     }
     const int ca = max(x0 - 1, 0), cb = min(x0 + ncol - 1, W);
-    a0[i] = (3ll * ((long long)r * W + ca)) & ~3ll;
-    const long long e = rin ? 3ll * ((long long)r * W + cb) : a0[i];
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const long long ad = a0[i] + 4ll * (tid + 256 * it);
-      uint32_t w = 0;
-      if (ad < e) {
-        if (aligned && ad + 4 <= nbytes) {
-          w = *reinterpret_cast<const uint32_t*>(ws.img + ad);
-        } else {
-          for (int k = 0; k < 4; ++k)
-            if (ad + k < nbytes) w |= (uint32_t)ws.img[ad + k] << (8 * k);
-        }
+    a0[i] = (3 * (r * W + ca)) & ~3;
+    const int e = rin ? 3 * (r * W + cb) : a0[i];
+    const int ad = a0[i] + 4 * tid;
+    uint32_t w = 0;
+    if (tid < PREP_RAW && ad < e) {
+      if (aligned && ad + 4 <= nbytes) {
+        w = *reinterpret_cast<const uint32_t*>(ws.img + ad);
+      } else {
+        for (int k = 0; k < 4; ++k)
+          if (ad + k < nbytes) w |= (uint32_t)ws.img[ad + k] << (8 * k);
       }
-      ireg[i][it] = w;
     }
+    ireg[i] = w;
   }
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
 #pragma unroll
-    for (int it = 0; it < 5; ++it) {
-      const int j = tid + 256 * it;
+    for (int it = 0; it < 2; ++it) {
+      const int j = tid + 1024 * it;
       if (j < ncol) s_m[i][j] = mreg[i][it];
     }
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int q = tid + 256 * it;
-      if (q < PREP_RAW) s_raw[i][q] = ireg[i][it];
-    }
+    if (tid < PREP_RAW) s_raw[i][tid] = ireg[i];
   }
   __syncthreads();
   const uint8_t* rawb = reinterpret_cast<const uint8_t*>(&s_raw[0][0]);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const int r = r0 - 1 + i;
-    for (int j = tid; j < ncol; j += 256) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int j = tid + 1024 * it;
+      if (j >= ncol) continue;
       const int c = x0 - 1 + j;
       uint32_t v = 0;
       if (r >= 0 && r < H && c >= 0 && c < W) {
-        const int o = (int)(3ll * ((long long)r * W + c) - a0[i]) + i * PREP_RAW * 4;
+        const int o = 3 * (r * W + c) - a0[i] + i * PREP_RAW * 4;
         v = (uint32_t)rawb[o] | ((uint32_t)rawb[o + 1] << 8) | ((uint32_t)rawb[o + 2] << 16);
       }
       s_px[i][j] = v;
     }
   }
   __syncthreads();
-  // ---- one tile per thread ----
-  const int tc = cs * (RSEG / 4) + tid;
+  // ---- one tile row per thread ----
+  const int tl = tid >> 2, ry = tid & 3;
+  const int tc = cs * (RSEG / 4) + tl;
+  const int r = r0 + ry, i = ry + 1;
+  unsigned p1mask = 0;  // bit rx: phase-1 pixel
   int run_w = -1;
   unsigned run_n = 0;
   auto cap_add = [&](int w) {
@@ -179,69 +180,64 @@ __global__ __launch_bounds__(256) void k_prep(Ws ws, const int32_t* __restrict__
     }
     ++run_n;
   };
-  unsigned p1mask = 0;            // bit 4*ry+rx: phase-1 pixel
-  unsigned long long rows4 = 0;   // 16-bit phase-1 counts of the 4 tile rows
   if (tc < Wt) {
-    const int c0 = tc * 4, jb = 4 * tid;  // strip column of c0 - 1
-    int4* out = reinterpret_cast<int4*>(ws.mk + ((((long long)tr * Wt + tc) << 4) << 1));
+    const int c0 = tc * 4, jb = 4 * tl;  // strip column of c0 - 1
+    int sv[4];
+    unsigned wv4[4];
 #pragma unroll
-    for (int ry = 0; ry < 4; ++ry) {
-      int sv[4];
-      unsigned wv4[4];
-#pragma unroll
-      for (int rx = 0; rx < 4; ++rx) {
-        const int r = r0 + ry, c = c0 + rx, i = ry + 1, j = jb + rx + 1;
-        int state = WSHED;
-        unsigned w4 = 0;
-        if (r < H && c < W) {
-          const uint32_t me = s_px[i][j];
-          const int wl = (c >= 1) ? cdiffp(me, s_px[i][j - 1]) : 0;
-          const int wr = (c + 1 < W) ? cdiffp(me, s_px[i][j + 1]) : 0;
-          const int wu = (r >= 1) ? cdiffp(me, s_px[i - 1][j]) : 0;
-          const int wd = (r + 1 < H) ? cdiffp(me, s_px[i + 1][j]) : 0;
-          w4 = (unsigned)wl | ((unsigned)wr << 8) | ((unsigned)wu << 16) | ((unsigned)wd << 24);
-          if (!(r == 0 || r == H - 1 || c == 0 || c == W - 1)) {
-            const int m = s_m[i][j];
-            if (m > 0) {
-              state = m;
+    for (int rx = 0; rx < 4; ++rx) {
+      const int c = c0 + rx, j = jb + rx + 1;
+      int state = WSHED;
+      unsigned w4 = 0;
+      if (r < H && c < W) {
+        const uint32_t me = s_px[i][j];
+        const int wl = (c >= 1) ? cdiffp(me, s_px[i][j - 1]) : 0;
+        const int wr = (c + 1 < W) ? cdiffp(me, s_px[i][j + 1]) : 0;
+        const int wu = (r >= 1) ? cdiffp(me, s_px[i - 1][j]) : 0;
+        const int wd = (r + 1 < H) ? cdiffp(me, s_px[i + 1][j]) : 0;
+        w4 = (unsigned)wl | ((unsigned)wr << 8) | ((unsigned)wu << 16) | ((unsigned)wd << 24);
+        if (!(r == 0 || r == H - 1 || c == 0 || c == W - 1)) {
+          const int m = s_m[i][j];
+          if (m > 0) {
+            state = m;
+          } else {
+            // interior neighbours (the frame is WSHED in the serial code and never counts)
+            const int wleft = (c >= 2) ? wl : -1;
+            const int wup = (r >= 2) ? wu : -1;
+            const int wr_i = (c <= W - 3) ? wr : -1;
+            const int wd_i = (r <= H - 3) ? wd : -1;
+            int lvl = 256;
+            if (wleft >= 0 && s_m[i][j - 1] > 0) lvl = min(lvl, wleft);
+            if (wr_i >= 0 && s_m[i][j + 1] > 0) lvl = min(lvl, wr_i);
+            if (wup >= 0 && s_m[i - 1][j] > 0) lvl = min(lvl, wup);
+            if (wd_i >= 0 && s_m[i + 1][j] > 0) lvl = min(lvl, wd_i);
+            if (lvl < 256) {
+              state = p1_state(lvl);
+              p1mask |= 1u << rx;
             } else {
-              // interior neighbours (the frame is WSHED in the serial code and never counts)
-              const int wleft = (c >= 2) ? wl : -1;
-              const int wup = (r >= 2) ? wu : -1;
-              const int wr_i = (c <= W - 3) ? wr : -1;
-              const int wd_i = (r <= H - 3) ? wd : -1;
-              int lvl = 256;
-              if (wleft >= 0 && s_m[i][j - 1] > 0) lvl = min(lvl, wleft);
-              if (wr_i >= 0 && s_m[i][j + 1] > 0) lvl = min(lvl, wr_i);
-              if (wup >= 0 && s_m[i - 1][j] > 0) lvl = min(lvl, wup);
-              if (wd_i >= 0 && s_m[i + 1][j] > 0) lvl = min(lvl, wd_i);
-              if (lvl < 256) {
-                state = p1_state(lvl);
-                p1mask |= 1u << (4 * ry + rx);
-                rows4 += 1ull << (16 * ry);
-              } else {
-                state = 0;
-              }
-              // this pixel may be queued once, at one of its distinct interior edge weights;
-              // run-length counted in registers (plateaus: one LDS atomic per thread, not per pixel)
-              if (wleft >= 0) cap_add(wleft);
-              if (wr_i >= 0 && wr_i != wleft) cap_add(wr_i);
-              if (wup >= 0 && wup != wleft && wup != wr_i) cap_add(wup);
-              if (wd_i >= 0 && wd_i != wleft && wd_i != wr_i && wd_i != wup) cap_add(wd_i);
+              state = 0;
             }
+            // this pixel may be queued once, at one of its distinct interior edge weights
+            if (wleft >= 0) cap_add(wleft);
+            if (wr_i >= 0 && wr_i != wleft) cap_add(wr_i);
+            if (wup >= 0 && wup != wleft && wup != wr_i) cap_add(wup);
+            if (wd_i >= 0 && wd_i != wleft && wd_i != wr_i && wd_i != wup) cap_add(wd_i);
           }
         }
-        sv[rx] = state;
-        wv4[rx] = w4;
       }
-      out[2 * ry] = make_int4(sv[0], (int)wv4[0], sv[1], (int)wv4[1]);
-      out[2 * ry + 1] = make_int4(sv[2], (int)wv4[2], sv[3], (int)wv4[3]);
+      sv[rx] = state;
+      wv4[rx] = w4;
     }
+    int4* out = reinterpret_cast<int4*>(ws.mk + ((((tr * Wt + tc) << 4) + 4 * ry) << 1));
+    out[0] = make_int4(sv[0], (int)wv4[0], sv[1], (int)wv4[1]);
+    out[1] = make_int4(sv[2], (int)wv4[2], sv[3], (int)wv4[3]);
   }
   if (run_n) atomicAdd(&caph[run_w], run_n);
-  // ---- phase-1 pixels of each of the 4 raster chunks, in raster order, into scratch at the
-  // chunk's raster offset in qbuf (read by k_compact; qbuf is filled only after it) ----
-  unsigned long long x = rows4;
+  // ---- phase-1 pixels of each of the 4 raster chunks (rows), in raster order, into scratch at
+  // the chunk's raster offset in qbuf (read by k_compact; qbuf is filled only after it):
+  // segmented exclusive scan, row ry's count in bits 16*ry of a 64-bit word ----
+  const unsigned long long mine = (unsigned long long)__popc(p1mask) << (16 * ry);
+  unsigned long long x = mine;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const unsigned long long y = __shfl_up(x, o);
@@ -249,22 +245,20 @@ __global__ __launch_bounds__(256) void k_prep(Ws ws, const int32_t* __restrict__
   }
   if (lane == 63) s_wsum[wv] = x;
   __syncthreads();
-  unsigned long long excl = x - rows4;
-  for (int k = 0; k < wv; ++k) excl += s_wsum[k];
-  const unsigned long long total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
-  if (p1mask) {
-    const long long t0 = ((long long)tr * Wt + tc) << 4;
-#pragma unroll
-    for (int ry = 0; ry < 4; ++ry) {
-      long long q = (long long)(r0 + ry) * W + x0 + (long long)((excl >> (16 * ry)) & 0xffff);
-#pragma unroll
-      for (int rx = 0; rx < 4; ++rx)
-        if ((p1mask >> (4 * ry + rx)) & 1u) ws.qbuf[q++] = (int32_t)(t0 + 4 * ry + rx);
-    }
+  unsigned long long excl = x - mine, total = 0;
+  for (int k = 0; k < 16; ++k) {
+    if (k < wv) excl += s_wsum[k];
+    total += s_wsum[k];
   }
-  if (caph[tid]) atomicAdd(&ws.capp[(blockIdx.x % CAP_SLOTS) * NQ + tid], caph[tid]);
-  if (tid < 4 && r0 + tid < H)
-    ws.tot[(long long)(r0 + tid) * ws.nseg + cs] = (int)((total >> (16 * tid)) & 0xffff);
+  if (p1mask) {
+    int q = r * W + x0 + (int)((excl >> (16 * ry)) & 0xffff);
+    const int t0 = ((tr * Wt + tc) << 4) + 4 * ry;
+#pragma unroll
+    for (int rx = 0; rx < 4; ++rx)
+      if ((p1mask >> rx) & 1u) ws.qbuf[q++] = t0 + rx;
+  }
+  if (tid < NQ && caph[tid]) atomicAdd(&ws.capp[(blockIdx.x % CAP_SLOTS) * NQ + tid], caph[tid]);
+  if (tid < 4 && r0 + tid < H) ws.tot[(r0 + tid) * ws.nseg + cs] = (int)((total >> (16 * tid)) & 0xffff);
 }
 
 // ---------------------------------------------------------------------------------------------
