@@ -53,7 +53,7 @@ typedef struct msg_stats {
     int64_t pushes;         /* queue appends after phase 1                                    */
     int64_t diag[8];        /* msg_set_diag counters (0 when off): k_resolve gather cycles,
                                dependency-loop cycles, loop rounds, max loop cycles, wave-rounds;
-                               k_small loop rounds, k_small launches that worked; reserved      */
+                               small-batch loop rounds, small-batch loop entries; reserved      */
 } msg_stats;
 
 #define MSG_NKERNELS 10
