@@ -9,7 +9,8 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmsegment.so")
+# MSEGMENT_LIB overrides the in-tree library (A/B timing of alternative builds of the same ABI)
+LIB_PATH = os.environ.get("MSEGMENT_LIB") or os.path.join(_HERE, "libmsegment.so")
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 MSG_OK = 0
