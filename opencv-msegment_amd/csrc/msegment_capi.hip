@@ -29,7 +29,8 @@ struct msg_ctx {
   Ctl* d_ctl = nullptr;
   // flood workspace (sized for cap_n pixels, cap_np tiled pixel words, cap_rc raster chunks)
   long long cap_n = 0, cap_np = 0, cap_rc = 0;
-  int32_t* d_px = nullptr;  // tiled {state, w4} words
+  int32_t* d_px_base = nullptr;  // tiled {state, w4} words, with a one-tile-row margin each side
+  int32_t* d_px = nullptr;       // = d_px_base + margin
   int32_t *d_qbuf = nullptr, *d_ilist = nullptr;
   int32_t *d_cnt = nullptr, *d_coff = nullptr, *d_tot = nullptr, *d_choff = nullptr;
   unsigned* d_capp = nullptr;  // CAP_SLOTS x NQ
@@ -133,7 +134,8 @@ void dfree(T*& p) {
 }
 
 void free_flood(msg_ctx* c) {
-  dfree(c->d_px);
+  dfree(c->d_px_base);
+  c->d_px = nullptr;
   dfree(c->d_qbuf); dfree(c->d_ilist);
   dfree(c->d_cnt); dfree(c->d_coff); dfree(c->d_tot); dfree(c->d_choff); dfree(c->d_capp);
   dfree(c->d_tl); dfree(c->d_desc);
@@ -146,16 +148,21 @@ void free_stage(msg_ctx* c) {
   c->stage_n = 0;
 }
 
+long long tile_margin(int W) { return 16ll * ((W + 3) / 4 + 1); }  // tiled words
+
 int ensure_flood(msg_ctx* c, int H, int W) {
   const long long N = (long long)H * W;
-  const long long Np = (long long)((H + 3) / 4) * ((W + 3) / 4) * 16;
+  // + a margin of one tile row (+ one tile) before and after: k_resolve's speculative
+  // radius-2 loads around frame-adjacent pixels may land there (values discarded)
+  const long long Np = (long long)((H + 3) / 4) * ((W + 3) / 4) * 16 + 2 * tile_margin(W);
   const long long nrc = (long long)H * ((W + RSEG - 1) / RSEG);
   if (N <= c->cap_n && Np <= c->cap_np && nrc <= c->cap_rc) return MSG_OK;
   const long long n = std::max(N, c->cap_n), np = std::max(Np, c->cap_np), rc = std::max(nrc, c->cap_rc);
   free_flood(c);
   const long long nch = (n + CH - 1) / CH;
   const long long qcap = 4 * n + 16;
-  HIPCHK(c, hipMalloc((void**)&c->d_px, np * 8));
+  HIPCHK(c, hipMalloc((void**)&c->d_px_base, np * 8));
+  HIPCHK(c, hipMemset(c->d_px_base, 0, np * 8));
   HIPCHK(c, hipMalloc((void**)&c->d_ilist, n * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_qbuf, qcap * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_tl, n * 8));
@@ -210,6 +217,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   }
   Ws ws;
   ws.img = d_img;
+  c->d_px = c->d_px_base + 2 * tile_margin(W);  // margin in words of 8 B = 2 ints
   ws.mk = c->d_px;
   ws.qbuf = c->d_qbuf;
   ws.ilist = c->d_ilist;

@@ -587,12 +587,21 @@ __device__ __forceinline__ void gather_item(const Ws& ws, const Seg* segs, int n
 #pragma unroll
   for (int k = 0; k < 16; ++k) it.dep[k] = -1;
   it.wts = ld_w4(ws, p);
+  // one round of loads for the whole radius-2 diamond: the 4 neighbours and, for each, its 3
+  // other neighbours (push competitors), needed only when the neighbour is a 0-pixel, i.e.
+  // interior; otherwise the value is discarded (the buffer has a one-tile-row margin either side)
   long long nb[4];
-  int v[4];
+  int v[4], vo[4][3];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     nb[d] = nb_of(p, d, Wt);
     v[d] = ld_state(ws, nb[d]);
+    const int e0 = (d == 1) ? 1 : 0;  // directions ascending, skipping the way back to p
+    const int e1 = (d <= 1) ? 2 : 1;
+    const int e2 = (d == 2) ? 2 : 3;
+    vo[d][0] = ld_state(ws, nb_of(nb[d], e0, Wt));
+    vo[d][1] = ld_state(ws, nb_of(nb[d], e1, Wt));
+    vo[d][2] = ld_state(ws, nb_of(nb[d], e2, Wt));
   }
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
@@ -609,17 +618,10 @@ __device__ __forceinline__ void gather_item(const Ws& ws, const Seg* segs, int n
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     if (!((it.zero_mask >> d) & 1u)) continue;
-    const long long n = nb[d];
-    // n's neighbours other than p (p is n's opposite-direction neighbour), directions ascending
-    const int e0 = (d == 1) ? 1 : 0;
-    const int e1 = (d <= 1) ? 2 : 1;
-    const int e2 = (d == 2) ? 2 : 3;
-    const long long o[3] = {nb_of(n, e0, Wt), nb_of(n, e1, Wt), nb_of(n, e2, Wt)};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const int vo = ld_state(ws, o[k]);
-      if (vo <= -3) {
-        const int r = rank_of_slot(segs, nseg, state_slot(vo));
+      if (vo[d][k] <= -3) {
+        const int r = rank_of_slot(segs, nseg, state_slot(vo[d][k]));
         if (r >= 0 && r < i) it.dep[4 + 3 * d + k] = r;
       }
     }
