@@ -128,6 +128,7 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--kind", default="mosaic", choices=["mosaic", "mosaic_noise", "random"])
+    ap.add_argument("--seed", type=int, default=None, help="default: 2 (N=1), 100+rank (N>1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile-pass", action="store_true")
     args = ap.parse_args(argv)
@@ -149,7 +150,7 @@ def main(argv=None):
     sync = torch.cuda.synchronize
 
     S = args.size
-    seed = 2 if world == 1 else 100 + rank
+    seed = args.seed if args.seed is not None else (2 if world == 1 else 100 + rank)
     t0 = time.perf_counter()
     img, m, depth = synth.frame(args.kind, S, S, seed)
     log("[rank %d] generated %s %dx%d seed %d in %.1fs" % (rank, args.kind, S, S, seed, time.perf_counter() - t0))
@@ -167,10 +168,12 @@ def main(argv=None):
     sync()
     st = seg.stats()
     parity = None
-    if rank == 0 and args.kind == "mosaic" and S == 4096 and seed == 2:
-        dg = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))["mosaic_4096x4096_s2"]
+    dgs = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
+    dkey = "%s_%dx%d_s%d" % (args.kind, S, S, seed)
+    if rank == 0 and dkey in dgs:  # committed oracle digest of this exact frame
         got = hashlib.sha256(t_lab.cpu().numpy().tobytes()).hexdigest()
-        parity = "bit-exact vs oracle digest" if got == dg["labels_sha256"] else "MISMATCH vs oracle digest"
+        parity = ("bit-exact vs oracle digest" if got == dgs[dkey]["labels_sha256"]
+                  else "MISMATCH vs oracle digest") + " " + dkey
         log("[rank 0] parity:", parity)
 
     dt = timed_steps(step, args.steps, barrier, sync)
@@ -234,7 +237,8 @@ def main(argv=None):
             "data": "synthetic (msegment.synth %s, splitmix64; regenerated on the box)" % args.kind,
             "config": {"workload": "%s %dx%d seed %s, watershed + colorByIndexes(colored=false), "
                                    "device-resident (BASELINE config %s)"
-                                   % (args.kind, S, S, "2" if world == 1 else "100+rank", "3" if world == 1 else "5"),
+                                   % (args.kind, S, S, seed if (world == 1 or args.seed is not None) else "100+rank",
+                                      {1024: "2", 16384: "4 frame on one GPU"}.get(S, "3") if world == 1 else "5"),
                        "frames_per_rank_per_step": 1, "parallelism": "replicas%d (no collectives)" % world},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -100,12 +100,24 @@ def main():
     arrays["__names"] = np.array(names)
     np.savez_compressed(os.path.join(OUT, "small_cases.npz"), **arrays)
 
-    digests = {}
-    for kind, H, W, seed in [("mosaic", 1024, 1024, 1), ("mosaic_noise", 1024, 1024, 1),
-                             ("random", 512, 512, 3), ("mosaic", 4096, 4096, 2)]:
+    write_digests()
+    print("wrote", len(names), "small cases")
+
+
+# (kind, H, W, seed): SURVEY.md §8d seeds -- cfg2 1024^2 s=1, cfg3 4096^2 s=2, cfg4 16384^2 s=3
+DIGEST_CASES = [("mosaic", 1024, 1024, 1), ("mosaic_noise", 1024, 1024, 1),
+                ("random", 512, 512, 3), ("mosaic", 4096, 4096, 2), ("mosaic", 16384, 16384, 3)]
+
+
+def write_digests(only=None):
+    path = os.path.join(OUT, "digests.json")
+    digests = json.load(open(path)) if (only and os.path.exists(path)) else {}
+    for kind, H, W, seed in DIGEST_CASES:
+        key = "%s_%dx%d_s%d" % (kind, H, W, seed)
+        if only and key not in only:
+            continue
         img, m, depth = synth.frame(kind, H, W, seed)
         lab = ws_oracle.watershed(img, m)
-        key = "%s_%dx%d_s%d" % (kind, H, W, seed)
         digests[key] = {
             "labels_sha256": hashlib.sha256(lab.tobytes()).hexdigest(),
             "img_sha256": hashlib.sha256(img.tobytes()).hexdigest(),
@@ -115,10 +127,13 @@ def main():
             "zero_pixels": int((lab == 0).sum()),
         }
         print(key, digests[key]["labels_sha256"][:16])
-    with open(os.path.join(OUT, "digests.json"), "w") as f:
+        del img, m, lab
+    with open(path, "w") as f:
         json.dump(digests, f, indent=1, sort_keys=True)
-    print("wrote", len(names), "small cases")
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "--digests-only":  # e.g. --digests-only mosaic_16384x16384_s3
+        write_digests(set(sys.argv[2:]) or None)
+    else:
+        main()

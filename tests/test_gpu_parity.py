@@ -118,6 +118,17 @@ def test_config3_4096_mosaic_digest_and_properties(seg):
     check_properties(m, out)
 
 
+def test_config4_16384_mosaic_digest_single_gpu(seg):
+    """BASELINE config 4's frame (16384^2, SURVEY.md seed 3) on ONE GPU: the 2^28-pixel frame's
+    ~12 GB workspace fits one MI355X (why it is not tile-sharded)."""
+    dg = json.load(open(os.path.join(GOLD, "digests.json")))["mosaic_16384x16384_s3"]
+    img, m, d = synth.frame("mosaic", 16384, 16384, 3)
+    out = gpu_ws(seg, img, m)
+    del img
+    assert hashlib.sha256(out.tobytes()).hexdigest() == dg["labels_sha256"]
+    assert int((out == -1).sum()) == dg["wshed_pixels"]
+
+
 def check_properties(m, out):
     """Size-independent watershed invariants."""
     H, W = m.shape
