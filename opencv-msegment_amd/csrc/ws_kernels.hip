@@ -1143,6 +1143,200 @@ __global__ __launch_bounds__(1024) void k_scatter(Ws ws) {
 // push decisions are pulled directly (an earlier non-WSHED batch item adjacent to the target
 // pushes it first) instead of claimed.  Exits, writing the queue state back, when the next batch
 // is larger than SMALL_MAX, the flood is done, or on error.
+// attempt_item with the dependencies' labels given per dependency slot (v[k] for it.dep[k]).
+__device__ __forceinline__ bool attempt_item_slots(const Item& it, const int (&v)[16], int& lab_out,
+                                                   unsigned& mask_out) {
+  int lab = it.base_lab;
+  bool unknown = false;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if (it.dep[d] < 0) continue;
+    if (v[d] == 0) unknown = true;
+    else if (v[d] > 0) lab = fold_lab(lab, v[d]);
+  }
+  if (lab == WSHED) {
+    lab_out = WSHED;
+    mask_out = 0;
+    return true;
+  }
+  if (unknown) return false;
+  unsigned m = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if (!((it.zero_mask >> d) & 1u)) continue;
+    bool lose = false, undecided = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (it.dep[4 + 3 * d + k] < 0) continue;
+      const int x = v[4 + 3 * d + k];
+      if (x > 0) lose = true;
+      else if (x == 0) undecided = true;
+    }
+    if (!lose) {
+      if (undecided) return false;
+      m |= 1u << d;
+    }
+  }
+  lab_out = lab;
+  mask_out = m;
+  return true;
+}
+
+// Tiny batches (<= 64 items), wave 0 only, no block barriers: item i on lane i, labels and push
+// decisions through register shuffles, the cut words through ballots, the ordered append through
+// wave_rank on the queue state the small loop keeps in LDS (in-order LDS within one wave).
+// Returns when the next batch has more than 64 items, the flood is done, or on error.
+constexpr int TINY_MAX = 64;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qbase, int* s_head, int* s_tail,
+                          int* wrow, int* s_wcap, int* s_err, int* s_nseg, int* s_n, long long* cnt) {
+  const int lane = lane_id();
+  const int Wt = ws.Wt;
+  for (;;) {
+    wave_sync();
+    const Batch B = *s_B;
+    if (B.n == 0 || B.mode != 0 || B.n > TINY_MAX || *s_err) return;
+    const int i = lane;
+    const bool valid = i < B.n;
+    Item it;
+    int sg = 0;
+    if (valid) {
+      sg = (B.nseg == 1) ? 0 : seg_of_rank(s_seg, B.nseg, i);
+      gather_item(ws, s_seg, B.nseg, i, s_seg[sg].bstart + (i - s_seg[sg].rank), it);
+    } else {
+      it.p = 0;
+      it.base_lab = WSHED;
+      it.zero_mask = 0;
+      it.wts = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) it.dep[k] = -1;
+    }
+    int mylab = 0;
+    unsigned mymask = 0;
+    bool done = !valid;
+    for (int round = 0; round <= TINY_MAX && __any(!done); ++round) {  // deps point to lower lanes
+      int snap[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) snap[k] = __shfl(mylab, it.dep[k] >= 0 ? it.dep[k] : lane);
+      if (!done) {
+        int lab;
+        unsigned m;
+        if (attempt_item_slots(it, snap, lab, m)) {
+          if (lab == 0) {  // impossible for an exact queue
+            *s_err = ERR_STATE;
+            lab = WSHED;
+          }
+          mylab = lab;
+          mymask = (lab == WSHED) ? 0u : m;
+          done = true;
+        }
+      }
+    }
+    if (__any(!done)) {
+      *s_err = ERR_STATE;
+      return;
+    }
+    // cut words: interrupt (push below the item's level) and segment cut, lowest level pushed
+    const int lvi = valid ? s_seg[sg].L : 0;
+    bool lower = false;
+    int tmin = NQ, mseg = NONE;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      if (!((mymask >> d) & 1u)) continue;
+      const int t = (int)((it.wts >> (8 * d)) & 255u);
+      if (t < lvi) lower = true;
+      else tmin = min(tmin, t);
+    }
+    if (tmin < NQ && B.nseg > 1) mseg = seg_cut_for(s_seg, B.nseg, sg, tmin);
+    const unsigned long long lowmask = __ballot(lower);
+    const int cut = lowmask ? (__ffsll((long long)lowmask) - 1) : NONE;
+    int minpush = lower ? 0 : tmin, segcut = mseg;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      minpush = min(minpush, __shfl_xor(minpush, o));
+      segcut = min(segcut, __shfl_xor(segcut, o));
+    }
+    int ncommit = B.n;
+    if (cut != NONE) ncommit = min(ncommit, cut + 1);
+    if (segcut != NONE) ncommit = min(ncommit, s_seg[segcut].rank);
+    // commit labels, ordered append of the committed pushes
+    const bool com = i < ncommit;
+    if (com) st_state(ws, it.p, mylab);
+    const unsigned mask = com ? mymask : 0u;
+    int pos[4] = {0, 0, 0, 0};
+    wave_rank(mask, it.wts, pos, wrow);  // wrow[level] = the wave's pushes at that level
+    wave_sync();
+    int pushed = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      if (!((mask >> d) & 1u)) continue;
+      const int lv = (it.wts >> (8 * d)) & 255;
+      const int dest = s_qbase[lv] + s_tail[lv] + pos[d];
+      if (dest < 0 || (long long)dest >= ws.qcap) {
+        *s_err = ERR_CAPACITY;
+        continue;
+      }
+      const long long n = nb_of(it.p, d, Wt);
+      st_state(ws, n, queued_state(dest));
+      ws.qbuf[dest] = (int32_t)n;
+      ++pushed;
+    }
+    wave_sync();
+    // tails += the wave's per-level totals (one lane per distinct level), rows back to zero
+    unsigned rem = mask;
+    for (;;) {
+      const unsigned long long act = __ballot(rem != 0);
+      if (act == 0) break;
+      const int leader = __ffsll((long long)act) - 1;
+      const int myl = rem ? (int)((it.wts >> (8 * (__ffs(rem) - 1))) & 255u) : -1;
+      const int lsel = __shfl(myl, leader);
+      if (lane == leader) {
+        s_tail[lsel] += wrow[lsel];
+        wrow[lsel] = 0;
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        if ((int)((it.wts >> (8 * d)) & 255u) == lsel) rem &= ~(1u << d);
+      wave_sync();
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pushed += __shfl_xor(pushed, o);
+    if (lane < B.nseg) {
+      const Seg s = s_seg[lane];
+      s_head[s.L] += max(0, min(ncommit - s.rank, s.n));
+    }
+    wave_sync();
+    const int wcap = next_wcap(*s_wcap, B.n, ncommit, cut != NONE && ncommit == cut + 1);
+    if (lane == 0) {
+      *s_wcap = wcap;
+      cnt[0] += ncommit;
+      cnt[1] += B.n;
+      cnt[2] += pushed;
+    }
+    wave_sync();
+    form_batch(s_qbase, s_head, s_tail, minpush, wcap, s_seg, s_nseg, s_n);
+    wave_sync();
+    if (lane == 0) {
+      Batch nb;
+      nb.mode = 0;
+      nb.epoch = B.epoch + 1;
+      nb.ncommit = 0;
+      nb.nchunk = 0;
+      nb.nseg = *s_nseg;
+      nb.n = (*s_nseg > 0) ? *s_n : 0;
+      nb.L = (*s_nseg > 0) ? s_seg[0].L : -1;
+      nb.bstart = (*s_nseg > 0) ? s_seg[0].bstart : 0;
+      *s_B = nb;
+      if (*s_nseg > 0) cnt[3] += 1;
+    }
+  }
+}
+
 __device__ __forceinline__ void small_loop(const Ws& ws) {
   constexpr int NW = 16;
   Ctl* ctl = ws.ctl;
@@ -1175,6 +1369,20 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     const Batch B = s_B;
     if (B.n == 0 || B.mode != 0 || B.n > SMALL_MAX || s_err) break;
     worked = true;
+    if (B.n <= TINY_MAX) {  // runs of tiny batches: wave 0 alone, the other waves wait here
+      if (wv == 0) {
+        long long c4[4] = {0, 0, 0, 0};
+        tiny_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, s_wcnt[0], &s_wcap, &s_err, &s_nseg, &s_n, c4);
+        if (tid == 0) {
+          nb_pops += c4[0];
+          nb_items += c4[1];
+          nb_push += c4[2];
+          nb_batches += c4[3];
+        }
+      }
+      __syncthreads();
+      continue;
+    }
     for (int k = tid; k < B.n; k += 1024) s_lab[k] = 0;
     if (tid == 0) {
       s_cut = NONE;

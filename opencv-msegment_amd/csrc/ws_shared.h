@@ -20,7 +20,7 @@ constexpr int RBS = 512;           // threads per k_resolve block (3 co-resident
 constexpr int SMALL_MAX = 4096;    // batches up to this size run inside the one-workgroup k_small
 constexpr int PAL_LDS_MAX = 16384; // palettes up to this many labels are staged in LDS
 constexpr int MERGE_CAP = 1 << 22; // largest multi-segment batch (items)
-constexpr int WMIN = 1024;         // smallest batch window (one small-loop round)
+constexpr int WMIN = 64;           // smallest batch window (one wave: the tiny-batch loop)
 // Batch window after committing ncommit of n items: an interrupt cut (a push below the item's
 // level) means the queue order is turning over fast, so the next batch is a short prefix; a
 // batch that filled its window uncut quadruples it.  Prefixes of the queue order: exact.
