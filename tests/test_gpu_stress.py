@@ -76,3 +76,13 @@ def test_synthetic_medium(seg, kind):
     for s in range(3):
         img, m, _ = synth.frame(kind, 384, 320, 40 + s, cells=16)
         _check(seg, img, m, "%s s%d" % (kind, s))
+
+
+@pytest.mark.parametrize("H,W", [(37, 2500), (5, 3077), (1029, 7), (130, 1025)])
+def test_wide_and_narrow_frames(seg, H, W):
+    """Several raster chunks per row (phase-1 compaction, RSEG = 1024 columns) with a partial last
+    one, partial 4x4 tiles on both axes, and single-tile-column frames."""
+    rng = np.random.default_rng(H * 7919 + W)
+    img = _terraced(rng, H, W, 4)
+    m = _markers(rng, H, W, 0.004, 9)
+    _check(seg, img, m, "shape %dx%d" % (H, W))
