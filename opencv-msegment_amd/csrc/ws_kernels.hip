@@ -94,13 +94,13 @@ constexpr int PREP_RAW = (3 * PREP_COLS + 8) / 4 + 1;  // dwords of one BGR row 
 
 // thread = one tile row (4 pixels): tile tid >> 2, row tid & 3, so 4 consecutive lanes write one
 // whole 128-B tile line; frames are <= 2^28 pixels, so 32-bit offsets (3N < 2^30) suffice.
-__global__ __launch_bounds__(1024) void k_prep(Ws ws, const int32_t* __restrict__ mk_in) {
-  static_assert(NQ == 256 && RSEG == 1024, "strip = 256 tiles x 4 rows = 1024 threads");
+__global__ __launch_bounds__(RSEG) void k_prep(Ws ws, const int32_t* __restrict__ mk_in) {
+  static_assert(RSEG >= NQ && RSEG % 64 == 0 && PREP_RAW <= RSEG, "strip = RSEG/4 tiles x 4 rows = RSEG threads");
   __shared__ unsigned caph[NQ];
   __shared__ uint32_t s_raw[6][PREP_RAW];
   __shared__ uint32_t s_px[6][PREP_LDW];
   __shared__ int32_t s_m[6][PREP_LDW];
-  __shared__ unsigned long long s_wsum[16];
+  __shared__ unsigned long long s_wsum[RSEG / 64];
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const int H = ws.H, W = ws.W, Wt = ws.Wt;
   const int tr = blockIdx.x / ws.nseg, cs = blockIdx.x % ws.nseg;
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(1024) void k_prep(Ws ws, const int32_t* __restrict_
     const bool rin = r >= 0 && r < H;
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
-      const int j = tid + 1024 * it, c = x0 - 1 + j;
+      const int j = tid + RSEG * it, c = x0 - 1 + j;
       mreg[i][it] = (rin && j < ncol && c >= 0 && c < W) ? mk_in[r * W + c] : 0;
     }
     const int ca = max(x0 - 1, 0), cb = min(x0 + ncol - 1, W);
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(1024) void k_prep(Ws ws, const int32_t* __restrict_
   for (int i = 0; i < 6; ++i) {
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
-      const int j = tid + 1024 * it;
+      const int j = tid + RSEG * it;
       if (j < ncol) s_m[i][j] = mreg[i][it];
     }
     if (tid < PREP_RAW) s_raw[i][tid] = ireg[i];
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(1024) void k_prep(Ws ws, const int32_t* __restrict_
     const int r = r0 - 1 + i;
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
-      const int j = tid + 1024 * it;
+      const int j = tid + RSEG * it;
       if (j >= ncol) continue;
       const int c = x0 - 1 + j;
       uint32_t v = 0;
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(1024) void k_prep(Ws ws, const int32_t* __restrict_
   if (lane == 63) s_wsum[wv] = x;
   __syncthreads();
   unsigned long long excl = x - mine, total = 0;
-  for (int k = 0; k < 16; ++k) {
+  for (int k = 0; k < RSEG / 64; ++k) {
     if (k < wv) excl += s_wsum[k];
     total += s_wsum[k];
   }
@@ -456,19 +456,61 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
     }
     if ((tid & 63) == 63) capw[tid >> 6] = cx;
   }
-  const int per = ((npxchunk + 1023) / 1024 + 3) & ~3;
-  const int a = min(npxchunk, tid * per), b = min(npxchunk, a + per);
-  long long s = 0;
-  if (b - a == per) {
-    for (int c = a; c < b; c += 4) {
-      const int4 v = *reinterpret_cast<const int4*>(ws.tot + c);
-      s += (long long)v.x + v.y + v.z + v.w;
+  // raster-chunk offsets: exclusive scan of the per-chunk phase-1 counts, 16 K chunks per pass
+  // (16 per thread, int4 loads/stores, in-register prefix, wave + block prefix, running carry)
+  const int lane = tid & 63, wv = tid >> 6;
+  long long carry = 0;
+  for (int c0 = 0; c0 < npxchunk; c0 += 1024 * 16) {
+    const int c = c0 + tid * 16;
+    int v[16];
+    if (c + 16 <= npxchunk) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int4 t = *reinterpret_cast<const int4*>(ws.tot + c + 4 * q);
+        v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = (c + q < npxchunk) ? ws.tot[c + q] : 0;
     }
-  } else {
-    for (int c = a; c < b; ++c) s += ws.tot[c];
+    long long s = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += v[q];
+    long long x = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const long long y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    long long off = carry + x - s;
+    long long tot = 0;
+    for (int k = 0; k < 16; ++k) {
+      if (k < wv) off += wsum[k];
+      tot += wsum[k];
+    }
+    int o16[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      o16[q] = (int)off;
+      off += v[q];
+    }
+    if (c + 16 <= npxchunk) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<int4*>(ws.choff + c + 4 * q) = make_int4(o16[4 * q], o16[4 * q + 1], o16[4 * q + 2], o16[4 * q + 3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (c + q < npxchunk) ws.choff[c + q] = o16[q];
+    }
+    carry += tot;
+    __syncthreads();  // wsum reused by the next pass
   }
+  if (tid == 0) total_items = carry;
   __syncthreads();
-  if (tid < NQ) {
+  if (tid < NQ) {  // bucket region bases (capw is visible after the barriers above)
     long long base = cx - cv;
     for (int k = 0; k < (tid >> 6); ++k) base += capw[k];
     ctl->qbase[tid] = (int)base;
@@ -477,29 +519,6 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
       ctl->qbase[NQ] = (int)min(acc, (long long)0x7fffffff);
       if (acc > ws.qcap) ctl->error = ERR_CAPACITY;
     }
-  }
-  const int lane = tid & 63, wv = tid >> 6;
-  long long x = s;
-  for (int o = 1; o < 64; o <<= 1) {
-    long long y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[wv] = x;
-  __syncthreads();
-  if (tid == 0) {
-    long long acc = 0;
-    for (int k = 0; k < 16; ++k) {
-      long long t = wsum[k];
-      wsum[k] = acc;
-      acc += t;
-    }
-    total_items = acc;
-  }
-  __syncthreads();
-  long long off = wsum[wv] + x - s;
-  for (int c = a; c < b; ++c) {
-    ws.choff[c] = (int)off;
-    off += ws.tot[c];
   }
   const long long M = total_items;
   if (tid == 0) {
@@ -521,22 +540,28 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
 }
 
 // Ordered compaction of the phase-1 pixels in raster order into ilist/desc + level histograms:
-// one wave per raster chunk copies the chunk's list (k_prep's scratch in qbuf) to its offset.
+// a wave takes 64 raster chunks, a lane copies one chunk's list (k_prep's scratch in qbuf).
 __device__ __forceinline__ int ld_state(const Ws& ws, long long t);
 
 __global__ __launch_bounds__(256) void k_compact(Ws ws, int nrc) {
   if (ws.ctl->bat.n == 0 || ws.ctl->bat.mode != 1) return;
   const int lane = lane_id();
-  const int ch = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (ch >= nrc) return;
-  const int n = ws.tot[ch];
-  if (n == 0) return;
-  const int r = ch / ws.nseg, cs = ch % ws.nseg;
-  const long long rs = (long long)r * ws.W + (long long)cs * RSEG;
-  const long long k0 = ws.choff[ch];
-  for (int j0 = 0; j0 < n; j0 += 64) {  // wave-uniform
-    const int j = j0 + lane;
-    const bool on = j < n;
+  const int ch0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;  // this wave's 64 raster chunks
+  if (ch0 >= nrc) return;
+  // lane = one raster chunk; all lanes copy their chunks' j-th pixels together
+  const int ch = ch0 + lane;
+  const int myn = (ch < nrc) ? ws.tot[ch] : 0;
+  long long rs = 0, k0 = 0;
+  if (myn > 0) {
+    const int r = ch / ws.nseg, cs = ch % ws.nseg;
+    rs = (long long)r * ws.W + (long long)cs * RSEG;
+    k0 = ws.choff[ch];
+  }
+  int nmax = myn;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o));
+  for (int j = 0; j < nmax; ++j) {  // wave-uniform
+    const bool on = j < myn;
     const long long k = k0 + j;
     long long bin = -1;
     if (on) {

@@ -36,7 +36,7 @@ constexpr long long SPIN_LIMIT_TICKS = 200000000ll;  // 2 s of s_memrealtime (10
 // line per tile), tiles row-major, Wt tiles per tile row.  A pixel and its 4 neighbours mostly
 // share a line, so a queue item costs ~2 random lines instead of ~4.
 constexpr int CAP_SLOTS = 64;  // spread of the capacity-histogram atomics (same-address contention)
-constexpr int RSEG = 1024;  // columns per raster chunk of the phase-1 compaction (256 tiles)
+constexpr int RSEG = 512;   // columns per raster chunk of the phase-1 compaction (128 tiles) = k_prep threads
 __host__ __device__ inline long long tix(int r, int c, int Wt) {
   return ((long long)((long long)(r >> 2) * Wt + (c >> 2)) << 4) | ((r & 3) << 2) | (c & 3);
 }
