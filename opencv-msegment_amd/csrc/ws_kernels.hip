@@ -989,13 +989,17 @@ __device__ Batch scan_body(const Ws& ws) {
   }
   const int oldt = (tid < NQ) ? s_tail[tid] : 0;
   column_scan(ws.cnt, ws.coff, nch, haspartial ? partial : nullptr, s_tail);
-  const int npush = block_sum((tid < NQ) ? s_tail[tid] - oldt : 0);
+  if (tid < NQ) {  // pushes appended: one atomic per wave of levels (no block barrier)
+    int dp = s_tail[tid] - oldt;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dp += __shfl_xor(dp, o);
+    if ((tid & 63) == 0 && dp) atomicAdd((unsigned long long*)&ctl->pushes, (unsigned long long)dp);
+  }
   if (B.mode == 0 && tid < B.nseg) {  // advance every segment's bucket head by what it committed
     const Seg s = s_seg[tid];
     s_head[s.L] += max(0, min(ncommit - s.rank, s.n));
   }
   if (tid == 0) {
-    ctl->pushes += npush;
     if (B.mode == 0) {
       ctl->pops += ncommit;
       ctl->items += B.n;
@@ -1036,9 +1040,16 @@ __device__ Batch scan_body(const Ws& ws) {
     if (ns > 0) ctl->batches += 1;
     else ctl->done = 1;
   }
-  const int q = block_sum(tid < NQ ? s_tail[tid] - s_head[tid] : 0);
-  if (tid == 0) ctl->remaining = q;
-  return s_cb;  // block_sum's barriers made s_cb visible
+  if (tid < 64) {  // queued items left (host polling hint): wave 0 alone
+    int q = 0;
+#pragma unroll
+    for (int k = 0; k < NQ / 64; ++k) q += s_tail[tid + 64 * k] - s_head[tid + 64 * k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    if (tid == 0) ctl->remaining = q;
+  }
+  __syncthreads();
+  return s_cb;  // visible after the barrier above
 }
 
 // Stable rank of this lane's pushes among the wave's pushes of the same level, in (lane, dir)
