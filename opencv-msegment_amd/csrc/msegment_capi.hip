@@ -65,10 +65,10 @@ struct msg_ctx {
 namespace {
 
 enum KernelId { KID_PREP, KID_INIT_SCAN, KID_COMPACT, KID_RESOLVE, KID_SCAN, KID_SCATTER,
-                KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_CLAIM };
+                KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_SPARE };
 const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_compact", "k_resolve",
                                                 "k_scan", "k_scatter", "k_colorize",
-                                                "k_edge_weights", "k_untile", "k_claim"};
+                                                "k_edge_weights", "k_untile", "(unused)"};
 
 hipEvent_t pool_event(msg_ctx* c) {
   if (c->evused == c->evpool.size()) {

@@ -16,14 +16,18 @@
 //     an ordered multi-bucket append (per-chunk level histograms -> column scan -> stable
 //     scatter), so every bucket stays in exact serial FIFO order.
 //
-// Data in HBM (N = rows*cols pixels, all dense row-major):
-//   mk   int32[N]  label state: >0 label, 0 unknown, -1 WSHED/frame, -2 queued (serial IN_QUEUE)
-//   wr,wd u8[N]    L-inf BGR distance to the right / lower neighbour (the colour-distance stencil)
-//   qpos int32[N]  absolute queue slot of a queued pixel (valid while mk == -2)
-//   qbuf int32[..] 256 bucket FIFOs, bucket L = qbuf[qbase[L] + head[L] .. qbase[L] + tail[L])
-//                  sized exactly by a per-level histogram of each pixel's distinct edge weights
-//   tl   u64[N]    per-rank {epoch, label} granule of the current batch (in-launch hand-off)
-//   desc u64[N]    per-rank push descriptor: mask (4 bits) << 32 | four 8-bit levels
+// Data in HBM (N = rows*cols pixels; details in DESIGN.md section 4):
+//   mk   u64[tiles*16] TILED flood words {state, w4}: 4x4-pixel tiles (one 128-B line each),
+//                  state >0 label, 0 unknown, -1 WSHED/frame, phase-1 marker, <= -3 queued at
+//                  slot -3-s; w4 = the four L-inf BGR distances to the L,R,T,B neighbours
+//   qbuf int32[..] 256 bucket FIFOs of tiled pixel indices, bucket L = qbuf[qbase[L] + head[L]
+//                  .. qbase[L] + tail[L]), sized exactly by a per-level histogram of each
+//                  pixel's distinct interior edge weights
+//   tl   u64[N]    per-rank granule of the current batch: {epoch, label} or provisional
+//   desc u64[N]    per-rank push descriptor: four 8-bit levels | mask << 32 | level | segment
+//   ipx  int32[N]  per-rank pixel
+// Per iteration: k_resolve (decide every item) -> k_scan (1 block: column scan, heads, next
+// batch; small batches run here) -> k_scatter (commit labels, ordered append).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -708,9 +712,7 @@ __device__ __forceinline__ bool attempt_item(const Item& it, F fetch, int& lab_o
 // spinning cannot deadlock.  In-wave dependencies go through register shuffles, others through
 // 8-byte granules {epoch, label} (final) or {epoch | bit 63, base fold} (provisional: a pending
 // dep whose settled neighbours fold to b can only end as b or WSHED).  Items then add their
-// pushes to the per-chunk level histograms and the cut words; the last block to finish (arrival
-// ticket) runs the scan, and when the committed batch is small also its scatter and the
-// small-batch loop.
+// pushes to the per-chunk level histograms and the cut words, which k_scan consumes.
 __device__ Batch scan_body(const Ws& ws);
 __device__ void scatter_chunks(const Ws& ws, const Batch& B, int first, int stride);
 __device__ __forceinline__ void small_loop(const Ws& ws);
@@ -1175,10 +1177,10 @@ __global__ __launch_bounds__(1024) void k_scatter(Ws ws) {
 // ---------------------------------------------------------------------------------------------
 // Small batches, one workgroup (16 waves), many batches per launch.  Runs of small batches
 // (interrupt cascades, generation tails) dominate the batch count; here each one costs a few
-// workgroup barriers instead of five kernel boundaries.  Labels of the batch live in LDS, so
-// push decisions are pulled directly (an earlier non-WSHED batch item adjacent to the target
-// pushes it first) instead of claimed.  Exits, writing the queue state back, when the next batch
-// is larger than SMALL_MAX, the flood is done, or on error.
+// workgroup barriers instead of three kernel boundaries.  Labels of the batch live in LDS and
+// push decisions are pulled (an earlier non-WSHED batch item adjacent to the target pushes it
+// first).  Exits, writing the queue state back, when the next batch is larger than SMALL_MAX,
+// the flood is done, or on error.
 // attempt_item with the dependencies' labels given per dependency slot (v[k] for it.dep[k]).
 __device__ __forceinline__ bool attempt_item_slots(const Item& it, const int (&v)[16], int& lab_out,
                                                    unsigned& mask_out) {

@@ -17,7 +17,7 @@ __host__ __device__ inline int queued_state(int slot) { return -3 - slot; }
 __host__ __device__ inline int state_slot(int state) { return -3 - state; }
 constexpr int NONE = 0x7fffffff;
 constexpr int RBS = 512;           // threads per k_resolve block (3 co-resident per CU)
-constexpr int SMALL_MAX = 4096;    // batches up to this size run inside the one-workgroup k_small
+constexpr int SMALL_MAX = 4096;    // batches up to this size run in k_scan's one-workgroup loop
 constexpr int PAL_LDS_MAX = 16384; // palettes up to this many labels are staged in LDS
 constexpr int MERGE_CAP = 1 << 22; // largest multi-segment batch (items)
 constexpr int WMIN = 64;           // smallest batch window (one wave: the tiny-batch loop)
@@ -88,13 +88,12 @@ struct Ctl {
   int qbase[NQ + 1];
   int qhead[NQ];
   int qtail[NQ];
-  Batch bat;    // current batch (written by k_init_scan / k_scan / k_small)
+  Batch bat;    // current batch (written by k_init_scan / k_scan, incl. its small-batch loop)
   Batch cbat;   // batch being committed by k_scatter (written by k_scan)
   Seg seg[NQ];  // segments of the current batch
   int cut;      // first rank of the current batch that pushes below its own level (NONE: none)
   int segcut;   // first segment invalidated by a push below its level (NONE: none)
   int minpush;  // lowest level pushed by the current batch (merge heuristic)
-  unsigned ticket;  // k_resolve blocks finished this iteration (the last one runs the scan)
   int wcap;         // batch window (0 = whole buckets): shrinks after interrupt cuts, regrows
   int done;
   int error;
