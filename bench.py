@@ -129,6 +129,11 @@ def main(argv=None):
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--kind", default="mosaic", choices=["mosaic", "mosaic_noise", "random"])
     ap.add_argument("--seed", type=int, default=None, help="default: 2 (N=1), 100+rank (N>1)")
+    ap.add_argument("--frames", type=int, default=1,
+                    help="frames per rank per step (BASELINE config 5: 64 frames over 8 GPUs = 8); "
+                         "default 1 = the headline single-frame step")
+    ap.add_argument("--inflight", type=int, default=8,
+                    help="floods kept in flight together when --frames > 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile-pass", action="store_true")
     args = ap.parse_args(argv)
@@ -159,9 +164,23 @@ def main(argv=None):
     t_lab = torch.empty_like(t_m)
     t_dst = torch.empty((S, S, 3), dtype=torch.uint8, device=dev)
     seg = msegment.Segmenter(local)
+    K = max(1, args.frames)
+    if K > 1:  # K frames (seeds seed..seed+K-1) per step, up to --inflight floods in flight
+        extra = [synth.frame(args.kind, S, S, seed + k) for k in range(1, K)]
+        b_img = [t_img] + [torch.from_numpy(f[0]).to(dev) for f in extra]
+        b_m = [t_m] + [torch.from_numpy(f[1]).to(dev) for f in extra]
+        b_lab = [t_lab] + [torch.empty_like(x) for x in b_m[1:]]
+        b_dst = [t_dst] + [torch.empty((S, S, 3), dtype=torch.uint8, device=dev) for _ in extra]
+        depth = max([depth] + [f[2] for f in extra])
+        seg.set_batch_inflight(args.inflight)
 
-    def step():
+    def step1():
         seg.watershed_colorize_dev(t_img, t_m, t_lab, depth, None, t_dst)
+
+    def stepk():
+        seg.watershed_colorize_batch_dev(b_img, b_m, b_lab, depth, None, b_dst)
+
+    step = step1 if K == 1 else stepk
 
     for _ in range(args.warmup):
         step()
@@ -178,7 +197,7 @@ def main(argv=None):
 
     dt = timed_steps(step, args.steps, barrier, sync)
     dt_max = reduce_max(dt, dev)
-    value = whole_job_mpx(world, S * S, args.steps, dt_max)
+    value = whole_job_mpx(world, K * S * S, args.steps, dt_max)
     ms_per_step = 1000.0 * dt_max / args.steps
     log("[rank %d] %.3f ms/step (max over ranks %.3f)" % (rank, 1000 * dt / args.steps, ms_per_step))
 
@@ -187,11 +206,11 @@ def main(argv=None):
         seg.set_profiling(True)
         seg.kernel_profile(reset=True)
         for _ in range(args.steps):
-            step()
+            step1()  # the kernels of one flood (batch sub-contexts are not instrumented)
         sync()
         prof = seg.kernel_profile(reset=True)
         seg.set_profiling(False)
-        kern = kernel_roofline(prof, st, S * S, args.steps)
+        kern = kernel_roofline(prof, st if K == 1 else seg.stats(), S * S, args.steps)
 
     pcie = None
     if rank == 0 and world == 1:
@@ -235,11 +254,13 @@ def main(argv=None):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (msegment.synth %s, splitmix64; regenerated on the box)" % args.kind,
-            "config": {"workload": "%s %dx%d seed %s, watershed + colorByIndexes(colored=false), "
+            "config": {"workload": "%s %dx%d seed %s%s, watershed + colorByIndexes(colored=false), "
                                    "device-resident (BASELINE config %s)"
                                    % (args.kind, S, S, seed if (world == 1 or args.seed is not None) else "100+rank",
-                                      {1024: "2", 16384: "4 frame on one GPU"}.get(S, "3") if world == 1 else "5"),
-                       "frames_per_rank_per_step": 1, "parallelism": "replicas%d (no collectives)" % world},
+                                      "" if K == 1 else "..+%d, %d floods in flight" % (K - 1, min(K, args.inflight)),
+                                      ({1024: "2", 16384: "4 frame on one GPU"}.get(S, "3") if K == 1
+                                       else "5 batching") if world == 1 else "5"),
+                       "frames_per_rank_per_step": K, "parallelism": "replicas%d (no collectives)" % world},
             "roofline": roof,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,

@@ -100,11 +100,16 @@ int msg_watershed_colorize(msg_ctx* ctx, const uint8_t* bgr, size_t bgr_stride,
                            int depth, const uint8_t* palette_bgr, uint8_t* dst_bgr,
                            size_t dst_stride, uint8_t* gray, size_t gray_stride);
 
-/* Batch of independent frames (BASELINE config 5): frames are processed back to back on this
- * context's device, no collectives.  Arrays have n entries. */
+/* Batch of independent frames (BASELINE config 5), no collectives: up to msg_set_batch_inflight
+ * floods run concurrently on this context's device (each on its own internal sub-context,
+ * stream and host thread; the floods are latency-bound, so they overlap).  Arrays have n
+ * entries.  Replaces: a loop of PictureService.watershed calls over frames. */
 int msg_watershed_batch(msg_ctx* ctx, int n, const uint8_t* const* bgr, const size_t* bgr_stride,
                         int32_t* const* markers, const size_t* marker_stride, const int* rows,
                         const int* cols);
+
+/* Floods kept in flight by the batch entry points (1..8, default 4; 1 = back to back). */
+int msg_set_batch_inflight(msg_ctx* ctx, int k);
 
 /* ---- device-resident entry points (dense layouts; pointers are device memory of the
  * context's device; stream = hipStream_t or NULL for the context's own stream).  They return
@@ -124,6 +129,15 @@ int msg_watershed_colorize_dev(msg_ctx* ctx, const void* d_bgr, const void* d_ma
 
 /* Stencil only: L-inf BGR distance to the right and lower neighbour (uint8 each, 0 past the
  * edge) -- the colour-distance kernel of the flood, exposed for parity tests and the roofline. */
+/* Device-resident batch of the fused call above (BASELINE config 5 on one GPU): frame k reads
+ * d_bgr[k], d_markers_in[k] and writes d_labels[k], d_dst_bgr[k] (rows[k] x cols[k]); one
+ * palette and depth for all.  The inputs must be complete on `stream` (it is synchronised
+ * first); returns when every frame's labels and colours are written. */
+int msg_watershed_colorize_batch_dev(msg_ctx* ctx, int n, const void* const* d_bgr,
+                                     const void* const* d_markers_in, void* const* d_labels,
+                                     const int* rows, const int* cols, int depth,
+                                     const void* d_palette_bgr, void* const* d_dst_bgr, void* stream);
+
 int msg_edge_weights_dev(msg_ctx* ctx, const void* d_bgr, void* d_wright, void* d_wdown,
                          int rows, int cols, void* stream);
 

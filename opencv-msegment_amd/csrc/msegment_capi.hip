@@ -14,6 +14,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -60,6 +61,11 @@ struct msg_ctx {
   std::vector<std::pair<int, size_t>> recs;  // (kernel id, index of the start event)
   double prof_ms[MSG_NKERNELS] = {};
   long long prof_n[MSG_NKERNELS] = {};
+  // batches: floods in flight (msg_set_batch_inflight) and the sub-contexts that run them, each
+  // with its own stream and workspace on this device (independent floods overlap: each is
+  // latency-bound), created on first use
+  int inflight = 4;
+  std::vector<msg_ctx*> subs;
 };
 
 namespace {
@@ -334,6 +340,85 @@ int upload_palette(msg_ctx* c, const uint8_t* pal, int depth, hipStream_t st) {
   return MSG_OK;
 }
 
+constexpr int MAX_INFLIGHT = 8;
+
+int ensure_subs(msg_ctx* c, int k) {
+  while ((int)c->subs.size() < k) {
+    msg_ctx* sub = nullptr;
+    const int rc = msg_create(&sub, c->dev, 0);
+    if (rc) return fail(c, rc, "batch sub-context creation failed (%d)", rc);
+    c->subs.push_back(sub);
+  }
+  return MSG_OK;
+}
+
+// fn(i, ctx) for frames i in [0, n): with inflight == 1 on c itself, else frame i on worker
+// i % inflight (one host thread per sub-context, the API's one-context-per-thread model).
+// Returns the first error, its text copied into c; stats = the sums over the frames.
+template <class F>
+int run_batch(msg_ctx* c, int n, F fn) {
+  const int k = std::max(1, std::min({c->inflight, n, MAX_INFLIGHT}));
+  msg_stats tot{};
+  auto add = [&tot](const msg_stats& s) {
+    tot.batches += s.batches;
+    tot.pops += s.pops;
+    tot.host_syncs += s.host_syncs;
+    tot.items += s.items;
+    tot.pushes += s.pushes;
+    tot.rows = s.rows;
+    tot.cols = s.cols;
+  };
+  if (k == 1) {
+    for (int i = 0; i < n; ++i) {
+      const int rc = fn(i, c);
+      if (rc) return rc;
+      add(c->stats);
+    }
+    c->stats = tot;
+    return MSG_OK;
+  }
+  int rc = ensure_subs(c, k);
+  if (rc) return rc;
+  std::vector<int> rcs(k, MSG_OK);
+  std::vector<msg_stats> st(k);
+  std::vector<std::thread> th;
+  for (int w = 0; w < k; ++w)
+    th.emplace_back([&, w]() {
+      msg_ctx* sub = c->subs[w];
+      if (hipSetDevice(c->dev) != hipSuccess) {
+        rcs[w] = MSG_EHIP;
+        return;
+      }
+      msg_stats acc{};
+      for (int i = w; i < n; i += k) {
+        const int r = fn(i, sub);
+        if (r) {
+          rcs[w] = r;
+          return;
+        }
+        acc.batches += sub->stats.batches;
+        acc.pops += sub->stats.pops;
+        acc.host_syncs += sub->stats.host_syncs;
+        acc.items += sub->stats.items;
+        acc.pushes += sub->stats.pushes;
+        acc.rows = sub->stats.rows;
+        acc.cols = sub->stats.cols;
+      }
+      if (hipStreamSynchronize(sub->own) != hipSuccess) rcs[w] = MSG_EHIP;
+      st[w] = acc;
+    });
+  for (auto& t : th) t.join();
+  for (int w = 0; w < k; ++w) {
+    if (rcs[w]) {
+      c->err = c->subs[w]->err.empty() ? std::string("batch worker failed") : c->subs[w]->err;
+      return rcs[w];
+    }
+    add(st[w]);
+  }
+  c->stats = tot;
+  return MSG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -379,6 +464,8 @@ void msg_destroy(msg_ctx* c) {
   (void)hipSetDevice(c->dev);
   if (c->own) (void)hipStreamSynchronize(c->own);
   free_flood(c);
+  for (msg_ctx* sub : c->subs) msg_destroy(sub);
+  c->subs.clear();
   free_stage(c);
   dfree(c->d_pal);
   dfree(c->d_ctl);
@@ -599,11 +686,31 @@ int msg_watershed_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size
   if (!c || n < 0) return MSG_EINVAL;
   if (n > 0 && (!bgr || !bgr_stride || !markers || !marker_stride || !rows || !cols))
     return fail(c, MSG_EINVAL, "null batch array");
-  for (int k = 0; k < n; ++k) {
-    int rc = msg_watershed(c, bgr[k], bgr_stride[k], markers[k], marker_stride[k], rows[k], cols[k]);
-    if (rc) return rc;
-  }
+  return run_batch(c, n, [&](int k, msg_ctx* x) {
+    return msg_watershed(x, bgr[k], bgr_stride[k], markers[k], marker_stride[k], rows[k], cols[k]);
+  });
+}
+
+int msg_set_batch_inflight(msg_ctx* c, int k) {
+  if (!c || k < 1) return MSG_EINVAL;
+  c->inflight = std::min(k, MAX_INFLIGHT);
   return MSG_OK;
+}
+
+int msg_watershed_colorize_batch_dev(msg_ctx* c, int n, const void* const* d_bgr,
+                                     const void* const* d_markers_in, void* const* d_labels,
+                                     const int* rows, const int* cols, int depth,
+                                     const void* d_palette_bgr, void* const* d_dst_bgr, void* stream) {
+  if (!c || n < 0) return MSG_EINVAL;
+  if (n > 0 && (!d_bgr || !d_markers_in || !d_labels || !rows || !cols || !d_dst_bgr))
+    return fail(c, MSG_EINVAL, "null batch array");
+  HIPCHK(c, hipSetDevice(c->dev));
+  // the inputs may still be in flight on the caller's stream: the floods run on other streams
+  HIPCHK(c, stream ? hipStreamSynchronize((hipStream_t)stream) : hipDeviceSynchronize());
+  return run_batch(c, n, [&](int k, msg_ctx* x) {
+    return msg_watershed_colorize_dev(x, d_bgr[k], d_markers_in[k], d_labels[k], rows[k], cols[k],
+                                      depth, d_palette_bgr, d_dst_bgr[k], nullptr, nullptr);
+  });
 }
 
 }  // extern "C"

@@ -165,6 +165,10 @@ class Segmenter:
             rows[k], cols[k] = m.shape
         self._check(self._L.msg_watershed_batch(self._h, n, bp, bs, mp, ms, rows, cols))
 
+    def set_batch_inflight(self, k):
+        """Floods kept in flight by the batch calls (1..8; 1 = back to back)."""
+        self._check(self._L.msg_set_batch_inflight(self._h, int(k)))
+
     # -- device-resident buffers (torch tensors on this device) ---------------------------
     @staticmethod
     def _stream(stream):
@@ -206,6 +210,21 @@ class Segmenter:
             ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(gray.data_ptr()) if gray is not None else None,
             self._stream(stream)))
         return dst
+
+    def watershed_colorize_batch_dev(self, bgrs, markers_in, labels, depth, palette, dsts, stream=None):
+        """Device-resident batch (BASELINE config 5 on one GPU): lists of torch tensors, frame k
+        reads bgrs[k], markers_in[k] and writes labels[k], dsts[k]; several floods in flight."""
+        n = len(bgrs)
+        if not (len(markers_in) == len(labels) == len(dsts) == n):
+            raise MsegError(_lib.MSG_EINVAL, "batch lists differ in length")
+        arr = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])  # noqa: E731
+        rows = (ctypes.c_int * n)(*[int(m.shape[0]) for m in markers_in])
+        cols = (ctypes.c_int * n)(*[int(m.shape[1]) for m in markers_in])
+        self._check(self._L.msg_watershed_colorize_batch_dev(
+            self._h, n, arr(bgrs), arr(markers_in), arr(labels), rows, cols, int(depth),
+            ctypes.c_void_p(palette.data_ptr()) if palette is not None else None, arr(dsts),
+            self._stream(stream)))
+        return dsts
 
     def edge_weights_dev(self, bgr, wright, wdown, stream=None):
         H, W = bgr.shape[:2]

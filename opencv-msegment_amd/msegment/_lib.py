@@ -26,6 +26,7 @@ EXPORTS = (
     "msg_watershed", "msg_colorize", "msg_watershed_colorize", "msg_watershed_batch",
     "msg_watershed_dev", "msg_colorize_dev", "msg_watershed_colorize_dev", "msg_edge_weights_dev",
     "msg_set_profiling", "msg_get_kernel_profile", "msg_set_diag",
+    "msg_set_batch_inflight", "msg_watershed_colorize_batch_dev",
 )
 
 
@@ -109,5 +110,9 @@ def load():
     L.msg_set_diag.restype = i
     L.msg_get_kernel_profile.argtypes = [vp, ctypes.POINTER(KernelProfile), i, i]
     L.msg_get_kernel_profile.restype = i
+    L.msg_set_batch_inflight.argtypes = [vp, i]
+    L.msg_set_batch_inflight.restype = i
+    L.msg_watershed_colorize_batch_dev.argtypes = [vp, i, vp, vp, vp, vp, vp, i, vp, vp, vp]
+    L.msg_watershed_colorize_batch_dev.restype = i
     _lib = L
     return L

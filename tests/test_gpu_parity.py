@@ -171,6 +171,46 @@ def test_batch_api(seg):
         assert np.array_equal(out, ws_oracle.watershed(img, m))
 
 
+@pytest.mark.parametrize("inflight", [1, 3, 8])
+def test_batch_api_inflight(seg, inflight):
+    """Several floods in flight (internal sub-contexts, one host thread each), frames of mixed
+    sizes and kinds; every frame bit-exact and written back to its own markers."""
+    frames = [synth.frame(("mosaic", "mosaic_noise")[k % 2], 60 + 17 * k, 90 + 5 * k, 200 + k)[:2]
+              for k in range(7)]
+    work = [(img, m.copy()) for img, m in frames]
+    seg.set_batch_inflight(inflight)
+    try:
+        seg.watershed_batch(work)
+    finally:
+        seg.set_batch_inflight(4)
+    for (img, m), (_, out) in zip(frames, work):
+        assert np.array_equal(out, ws_oracle.watershed(img, m))
+
+
+def test_batch_dev_inflight(seg):
+    import torch
+
+    dev = torch.device("cuda", seg.device)
+    frames = [synth.frame(("mosaic", "mosaic_noise", "random")[k % 3], 100 + 31 * k, 140 - 9 * k, 300 + k)
+              for k in range(6)]
+    depth = max(f[2] for f in frames)
+    pal = generate_bgr_palette(depth, 11)
+    t_pal = torch.from_numpy(pal).to(dev)
+    bgrs = [torch.from_numpy(f[0]).to(dev) for f in frames]
+    mks = [torch.from_numpy(f[1]).to(dev) for f in frames]
+    labs = [torch.empty_like(m) for m in mks]
+    dsts = [torch.empty((m.shape[0], m.shape[1], 3), dtype=torch.uint8, device=dev) for m in mks]
+    seg.set_batch_inflight(3)
+    try:
+        seg.watershed_colorize_batch_dev(bgrs, mks, labs, depth, t_pal, dsts)
+    finally:
+        seg.set_batch_inflight(4)
+    for f, lab, dst in zip(frames, labs, dsts):
+        want = ws_oracle.watershed(f[0], f[1])
+        assert np.array_equal(lab.cpu().numpy(), want)
+        assert np.array_equal(dst.cpu().numpy(), ws_oracle.colorize(want, depth, pal))
+
+
 def test_colorize_palette_sizes(seg):
     rng = np.random.default_rng(3)
     for depth in [0, 1, 7, 5000, 20000, 70000]:
