@@ -225,6 +225,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   ws.img = d_img;
   c->d_px = c->d_px_base + 2 * tile_margin(W);  // margin in words of 8 B = 2 ints
   ws.mk = c->d_px;
+  ws.marg = (int)tile_margin(W);
   ws.qbuf = c->d_qbuf;
   ws.ilist = c->d_ilist;
   ws.tl = c->d_tl;

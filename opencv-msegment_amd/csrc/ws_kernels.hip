@@ -588,6 +588,16 @@ __global__ __launch_bounds__(256) void k_compact(Ws ws, int nrc) {
 }
 
 __device__ __forceinline__ int ld_state(const Ws& ws, long long t) { return ws.mk[t << 1]; }
+// 32-bit form of nb_of for indices taken from the margin start (a multiple of 16: tile-aligned)
+__device__ __forceinline__ int nbi(int t, int d, int Wt) {
+  const int row = Wt << 4;
+  switch (d) {
+    case 0: return (t & 3) ? t - 1 : t - 13;
+    case 1: return ((t & 3) != 3) ? t + 1 : t + 13;
+    case 2: return (t & 12) ? t - 4 : t - row + 12;
+    default: return ((t & 12) != 12) ? t + 4 : t + row - 12;
+  }
+}
 __device__ __forceinline__ void st_state(const Ws& ws, long long t, int v) { ws.mk[t << 1] = v; }
 __device__ __forceinline__ unsigned ld_w4(const Ws& ws, long long t) {
   return (unsigned)ws.mk[(t << 1) | 1];
@@ -618,19 +628,21 @@ __device__ __forceinline__ void gather_item(const Ws& ws, const Seg* segs, int n
   it.wts = ld_w4(ws, p);
   // one round of loads for the whole radius-2 diamond: the 4 neighbours and, for each, its 3
   // other neighbours (push competitors), needed only when the neighbour is a 0-pixel, i.e.
-  // interior; otherwise the value is discarded (the buffer has a one-tile-row margin either side)
-  long long nb[4];
+  // interior; otherwise the value is discarded (the buffer has a one-tile-row margin either side).
+  // Offsets are taken from the margin's start, so they are non-negative and fit 32 bits.
+  const int32_t* const mkb = ws.mk - 2 * (long long)ws.marg;
+  const int pb = p + ws.marg;  // tiled index relative to the margin start
   int v[4], vo[4][3];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    nb[d] = nb_of(p, d, Wt);
-    v[d] = ld_state(ws, nb[d]);
+    const int n = nbi(pb, d, Wt);
+    v[d] = mkb[(unsigned)n << 1];
     const int e0 = (d == 1) ? 1 : 0;  // directions ascending, skipping the way back to p
     const int e1 = (d <= 1) ? 2 : 1;
     const int e2 = (d == 2) ? 2 : 3;
-    vo[d][0] = ld_state(ws, nb_of(nb[d], e0, Wt));
-    vo[d][1] = ld_state(ws, nb_of(nb[d], e1, Wt));
-    vo[d][2] = ld_state(ws, nb_of(nb[d], e2, Wt));
+    vo[d][0] = mkb[(unsigned)nbi(n, e0, Wt) << 1];
+    vo[d][1] = mkb[(unsigned)nbi(n, e1, Wt) << 1];
+    vo[d][2] = mkb[(unsigned)nbi(n, e2, Wt) << 1];
   }
 #pragma unroll
   for (int d = 0; d < 4; ++d) {

@@ -121,6 +121,7 @@ struct Ws {
   unsigned long long* diag;  // nullptr = off; else 8 counters (msg_set_diag)
   int H, W;
   int Wt;            // tiles per tile row = ceil(W / 4)
+  int marg;          // tiled words of margin before mk (mk - 2*marg is the allocation start)
   int nseg;          // raster chunks per image row = ceil(W / RSEG)
   long long N;
   long long qcap;
