@@ -38,9 +38,12 @@ extern "C" {
 #define MSG_EHIP     (-2)  /* a HIP runtime call failed                                    */
 #define MSG_ENOMEM   (-3)  /* device allocation failed                                     */
 #define MSG_ETIMEOUT (-4)  /* a bounded in-kernel wait expired (result invalid)            */
-#define MSG_ESTATE   (-5)  /* internal consistency check failed on the device              */
+#define MSG_ESTATE   (-5)  /* internal consistency check failed on the device, or a state
+                              the reference itself fails in (documented per entry point)   */
+#define MSG_ERANGE   (-6)  /* output array too small / search space beyond what the
+                              reference could finish (documented per entry point)          */
 
-#define MSG_ABI_VERSION 1
+#define MSG_ABI_VERSION 2
 
 typedef struct msg_ctx msg_ctx;
 
@@ -56,7 +59,7 @@ typedef struct msg_stats {
                                small-batch loop rounds, small-batch loop entries; reserved      */
 } msg_stats;
 
-#define MSG_NKERNELS 10
+#define MSG_NKERNELS 12
 typedef struct msg_kernel_profile {
     char    name[32];       /* kernel name, e.g. "k_resolve"                                   */
     int64_t launches;       /* launches timed since the last reset                              */
@@ -127,8 +130,6 @@ int msg_watershed_colorize_dev(msg_ctx* ctx, const void* d_bgr, const void* d_ma
                                const void* d_palette_bgr, void* d_dst_bgr, void* d_gray,
                                void* stream);
 
-/* Stencil only: L-inf BGR distance to the right and lower neighbour (uint8 each, 0 past the
- * edge) -- the colour-distance kernel of the flood, exposed for parity tests and the roofline. */
 /* Device-resident batch of the fused call above (BASELINE config 5 on one GPU): frame k reads
  * d_bgr[k], d_markers_in[k] and writes d_labels[k], d_dst_bgr[k] (rows[k] x cols[k]); one
  * palette and depth for all.  The inputs must be complete on `stream` (it is synchronised
@@ -138,8 +139,57 @@ int msg_watershed_colorize_batch_dev(msg_ctx* ctx, int n, const void* const* d_b
                                      const int* rows, const int* cols, int depth,
                                      const void* d_palette_bgr, void* const* d_dst_bgr, void* stream);
 
+/* Stencil only: L-inf BGR distance to the right and lower neighbour (uint8 each, 0 past the
+ * edge) -- the colour-distance kernel of the flood, exposed for parity tests and the roofline. */
 int msg_edge_weights_dev(msg_ctx* ctx, const void* d_bgr, void* d_wright, void* d_wdown,
                          int rows, int cols, void* stream);
+
+/* ---- NOT_CONNECTED_MARKERS marker stage: the caller that builds the flood's seeds in
+ * PictureService.notConnectedMarkers (PictureService.java:468-842).  Dense device layouts;
+ * d_bgr and d_gray need 4-byte alignment, d_markers 16-byte alignment. ------------------- */
+
+#define MSG_NC_GISTO_DIAP 0x1u  /* AlgorithmOptions.GISTO_DIAP: mark the +-3 band around a
+                                   level's mean instead of the mean alone (:799-808)        */
+#define MSG_NC_MULTI_OTSU 0x2u  /* AlgorithmOptions.MULTI_OTSU: replace the levels by the
+                                   multi-Otsu split of the 128-bin histogram (:650-722)     */
+
+typedef struct msg_bright_level {  /* model/BrightLevel.java */
+    int32_t start, end, count;
+} msg_bright_level;
+
+/* srcGray = cvtColor(src, COLOR_BGR2GRAY) (:476-478) into d_gray (rows*cols bytes) and its
+ * 256-bin histogram calcHist(srcGray, [0,256)) (:565) into hist256 (HOST, exact counts).
+ * Returns when hist256 is filled. */
+int msg_gray_hist_dev(msg_ctx* ctx, const void* d_bgr, int rows, int cols, void* d_gray,
+                      int32_t* hist256, void* stream);
+
+/* Host only (no context, no GPU): the brightness levels of notConnectedMarkers from the
+ * histogram -- the flex thresholds (:574-640), or with MSG_NC_MULTI_OTSU the multi-Otsu
+ * override (:650-722; the reference's recursion enumerates ~C(128,k) splits for k flex levels:
+ * MSG_ERANGE when that exceeds 2e9 iterations, which it could not finish either).  depth is
+ * the user's depth (block size limit 256/depth).  Writes min(n, max_levels) levels and n;
+ * MSG_ERANGE if n > max_levels; MSG_ESTATE where the reference throws (no level at all);
+ * MSG_EINVAL for depth <= 0 (ArithmeticException). */
+int msg_nc_levels(const int32_t* hist256, int rows, int cols, int depth, unsigned options,
+                  msg_bright_level* levels, int max_levels, int* n_levels);
+
+/* Host only: brightness -> marker table of "ALLOCATE TO LAYERS" (:781-828): lut256[b] = 1 + the
+ * index of the first level whose mean (GISTO_DIAP: mean band) holds b, else 0. */
+int msg_nc_marker_lut(const msg_bright_level* levels, int n_levels, unsigned options,
+                      int32_t* lut256);
+
+/* markers(i,j) = lut256[gray(i,j)] into d_markers (int32, rows*cols): the summed marker maps
+ * wshedMarkSumm (:823-828) that PictureService.watershed then floods (:834). */
+int msg_nc_markers_dev(msg_ctx* ctx, const void* d_gray, int rows, int cols,
+                       const int32_t* lut256, void* d_markers, void* stream);
+
+/* The whole marker stage: gray + histogram -> levels -> markers.  d_gray may be NULL (context
+ * scratch).  The level count is the watershed depth the reference then uses (:834): draw the
+ * palettes for it and call msg_watershed_colorize_dev(d_bgr, d_markers, ...). */
+int msg_nc_marker_stage_dev(msg_ctx* ctx, const void* d_bgr, int rows, int cols, int depth,
+                            unsigned options, void* d_gray, void* d_markers,
+                            msg_bright_level* levels, int max_levels, int* n_levels,
+                            void* stream);
 
 #ifdef __cplusplus
 }

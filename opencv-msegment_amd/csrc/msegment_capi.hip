@@ -20,6 +20,7 @@
 
 #include "../../include/msegment.h"
 #include "ws_kernels.hip"
+#include "nc_kernels.hip"
 
 using namespace msg;
 
@@ -66,15 +67,22 @@ struct msg_ctx {
   // latency-bound), created on first use
   int inflight = 4;
   std::vector<msg_ctx*> subs;
+  // marker stage: device histogram + its pinned host mirror, gray scratch
+  int cus = 0;
+  unsigned* d_hist = nullptr;  // 256 bins
+  unsigned* h_hist = nullptr;
+  uint8_t* d_gscr = nullptr;
+  long long gscr_n = 0;
 };
 
 namespace {
 
 enum KernelId { KID_PREP, KID_INIT_SCAN, KID_COMPACT, KID_RESOLVE, KID_SCAN, KID_SCATTER,
-                KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_SPARE };
+                KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_GRAY_HIST, KID_NC_MARKERS, KID_SPARE };
 const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_compact", "k_resolve",
                                                 "k_scan", "k_scatter", "k_colorize",
-                                                "k_edge_weights", "k_untile", "(unused)"};
+                                                "k_edge_weights", "k_untile", "k_gray_hist",
+                                                "k_nc_markers", "(unused)"};
 
 hipEvent_t pool_event(msg_ctx* c) {
   if (c->evused == c->evpool.size()) {
@@ -420,6 +428,48 @@ int run_batch(msg_ctx* c, int n, F fn) {
   return MSG_OK;
 }
 
+// Streaming-kernel grid: enough 256-thread blocks for ~4 waves of 4-pixel groups per SIMD.
+int stream_grid(long long N) {
+  const long long th = (N + 3) / 4;
+  return (int)std::max<long long>(1, std::min<long long>((th + 255) / 256, 4096));
+}
+
+bool aligned(const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
+
+int gray_hist(msg_ctx* c, const uint8_t* d_bgr, long long N, uint8_t* d_gray, int32_t* hist,
+              hipStream_t st) {
+  if (!c->d_hist) {
+    HIPCHK(c, hipMalloc((void**)&c->d_hist, 256 * sizeof(unsigned)));
+    HIPCHK(c, hipHostMalloc((void**)&c->h_hist, 256 * sizeof(unsigned), hipHostMallocDefault));
+  }
+  if (N == 0) {
+    for (int i = 0; i < 256; ++i) hist[i] = 0;
+    return MSG_OK;
+  }
+  HIPCHK(c, hipMemsetAsync(c->d_hist, 0, 256 * sizeof(unsigned), st));
+  // one block per CU (fewer when the frame is small)
+  const long long per_block = (long long)GH_BS * GH_UNROLL;
+  const int grid = (int)std::max<long long>(1, std::min<long long>(c->cus, ((N >> 2) + per_block - 1) / per_block));
+  LAUNCH(c, KID_GRAY_HIST, st, k_gray_hist, dim3(grid), dim3(GH_BS), 0, d_bgr, N, d_gray, c->d_hist);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->h_hist, c->d_hist, 256 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  if (c->prof) collect_profile(c);
+  for (int i = 0; i < 256; ++i) hist[i] = (int32_t)c->h_hist[i];
+  return MSG_OK;
+}
+
+int nc_markers(msg_ctx* c, const uint8_t* d_gray, long long N, const int32_t* lut, int32_t* d_markers,
+               hipStream_t st) {
+  if (N == 0) return MSG_OK;
+  NcLut L;
+  std::memcpy(L.v, lut, sizeof(L.v));
+  LAUNCH(c, KID_NC_MARKERS, st, k_nc_markers, dim3(stream_grid(N)), dim3(256), 0, d_gray, N,
+         d_markers, L);
+  HIPCHK(c, hipGetLastError());
+  return MSG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -455,6 +505,7 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
     // blocks of a k_resolve round wait on each other, so the grid must be co-resident: the
     // occupancy answer (3 x 512 threads per CU at k_resolve's 80 VGPRs), capped at 4
     c->res_grid = cus * std::max(1, std::min(per, 4));
+    c->cus = cus;
   }
   *out = c;
   return MSG_OK;
@@ -471,6 +522,9 @@ void msg_destroy(msg_ctx* c) {
   dfree(c->d_pal);
   dfree(c->d_ctl);
   dfree(c->d_diag);
+  dfree(c->d_hist);
+  dfree(c->d_gscr);
+  if (c->h_hist) (void)hipHostFree(c->h_hist);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
@@ -712,6 +766,84 @@ int msg_watershed_colorize_batch_dev(msg_ctx* c, int n, const void* const* d_bgr
     return msg_watershed_colorize_dev(x, d_bgr[k], d_markers_in[k], d_labels[k], rows[k], cols[k],
                                       depth, d_palette_bgr, d_dst_bgr[k], nullptr, nullptr);
   });
+}
+
+int msg_gray_hist_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, void* d_gray,
+                      int32_t* hist256, void* stream) {
+  if (!c) return MSG_EINVAL;
+  int rc = check_size(c, rows, cols);
+  if (rc) return rc;
+  if (!hist256) return fail(c, MSG_EINVAL, "null histogram pointer");
+  const long long N = (long long)rows * cols;
+  if (N > 0 && (!d_bgr || !d_gray)) return fail(c, MSG_EINVAL, "null device pointer");
+  if (!aligned(d_bgr, 4) || !aligned(d_gray, 4))
+    return fail(c, MSG_EINVAL, "d_bgr and d_gray must be 4-byte aligned");
+  HIPCHK(c, hipSetDevice(c->dev));
+  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  return gray_hist(c, (const uint8_t*)d_bgr, N, (uint8_t*)d_gray, hist256, st);
+}
+
+int msg_nc_markers_dev(msg_ctx* c, const void* d_gray, int rows, int cols, const int32_t* lut256,
+                       void* d_markers, void* stream) {
+  if (!c) return MSG_EINVAL;
+  int rc = check_size(c, rows, cols);
+  if (rc) return rc;
+  if (!lut256) return fail(c, MSG_EINVAL, "null marker table");
+  const long long N = (long long)rows * cols;
+  if (N > 0 && (!d_gray || !d_markers)) return fail(c, MSG_EINVAL, "null device pointer");
+  if (!aligned(d_gray, 4) || !aligned(d_markers, 16))
+    return fail(c, MSG_EINVAL, "d_gray must be 4-byte and d_markers 16-byte aligned");
+  HIPCHK(c, hipSetDevice(c->dev));
+  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  return nc_markers(c, (const uint8_t*)d_gray, N, lut256, (int32_t*)d_markers, st);
+}
+
+int msg_nc_marker_stage_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, int depth,
+                            unsigned options, void* d_gray, void* d_markers,
+                            msg_bright_level* levels, int max_levels, int* n_levels,
+                            void* stream) {
+  if (!c) return MSG_EINVAL;
+  int rc = check_size(c, rows, cols);
+  if (rc) return rc;
+  if (!n_levels || (max_levels > 0 && !levels)) return fail(c, MSG_EINVAL, "null level array");
+  *n_levels = 0;
+  if (depth <= 0) return fail(c, MSG_EINVAL, "depth must be positive (256 / depth)");
+  const long long N = (long long)rows * cols;
+  if (N > 0 && (!d_bgr || !d_markers)) return fail(c, MSG_EINVAL, "null device pointer");
+  if (!aligned(d_bgr, 4) || !aligned(d_gray, 4) || !aligned(d_markers, 16))
+    return fail(c, MSG_EINVAL, "d_bgr/d_gray must be 4-byte and d_markers 16-byte aligned");
+  HIPCHK(c, hipSetDevice(c->dev));
+  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  uint8_t* g = (uint8_t*)d_gray;
+  if (!g && N > 0) {
+    if (c->gscr_n < N) {
+      dfree(c->d_gscr);
+      c->gscr_n = 0;
+      HIPCHK(c, hipMalloc((void**)&c->d_gscr, N + 16));
+      c->gscr_n = N;
+    }
+    g = c->d_gscr;
+  }
+  int32_t hist[256];
+  rc = gray_hist(c, (const uint8_t*)d_bgr, N, g, hist, st);
+  if (rc) return rc;
+  int n = 0;
+  std::vector<msg_bright_level> all(256);  // at most one level closes per bin 1..255
+  rc = msg_nc_levels(hist, rows, cols, depth, options, all.data(), (int)all.size(), &n);
+  if (rc == MSG_ERANGE && n == 0)
+    return fail(c, MSG_ERANGE, "multi-Otsu search space too large (the reference's otsuPart "
+                               "enumerates ~C(128, k) splits)");
+  if (rc == MSG_ESTATE)
+    return fail(c, MSG_ESTATE, "no brightness level (the reference throws here)");
+  if (rc) return fail(c, rc, "level computation failed (%d)", rc);
+  int32_t lut[256];
+  msg_nc_marker_lut(all.data(), n, options, lut);
+  rc = nc_markers(c, g, N, lut, (int32_t*)d_markers, st);
+  if (rc) return rc;
+  for (int i = 0; i < n && i < max_levels; ++i) levels[i] = all[i];
+  *n_levels = n;
+  if (n > max_levels) return fail(c, MSG_ERANGE, "%d levels, array holds %d", n, max_levels);
+  return MSG_OK;
 }
 
 }  // extern "C"

@@ -1,0 +1,124 @@
+// nc_kernels.hip -- gfx950 kernels of the NOT_CONNECTED_MARKERS marker stage, the caller that
+// builds the flood's seeds in PictureService.notConnectedMarkers (PictureService.java:468-842):
+//
+//   srcGray = cvtColor(src, COLOR_BGR2GRAY)                          :476-478
+//   brightHist = calcHist(srcGray, 256 bins, [0, 256))               :565
+//   ... levels from the histogram (host, nc_levels.cpp)               :574-722
+//   markers(i,j) = idx of the first level whose mean (or mean band)  :781-842
+//                  equals srcGray(i,j), else 0; summed over the level maps (one term is nonzero)
+//
+// Both kernels stream: k_gray_hist reads 3 B/px and writes 1 B/px (+ 256 atomics per block),
+// k_nc_markers reads 1 B/px and writes 4 B/px.  One thread = four pixels (three dword loads of
+// BGR, one dword of gray), grid-strided, so 4-byte alignment of the frame buffers is required
+// (checked on the host); markers are stored as int4, so that buffer needs 16-byte alignment.
+// Plain (temporal) loads and stores: the flood that follows re-reads the frame and the markers,
+// and at 4096^2 they fit the 256 MB MALL.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace msg {
+
+constexpr int GH_BS = 1024;   // k_gray_hist block (16 waves), one block per CU
+constexpr int GH_COPIES = 2;  // LDS sub-histograms per wave (lane & 1), rows padded to 257 words
+constexpr int GH_UNROLL = 4;  // 4-pixel groups per thread in flight (4 x 12 B loads)
+
+// OpenCV's 8-bit BGR2GRAY (fixed point, yuv_shift 14): Y = (1868 B + 9617 G + 4899 R + 2^13) >> 14
+__device__ __forceinline__ uint32_t gray_of(uint32_t b, uint32_t g, uint32_t r) {
+  return (1868u * b + 9617u * g + 4899u * r + 8192u) >> 14;
+}
+
+// Counts go to LDS sub-histograms (two per wave, rows skewed by one bank so the copies of a bin
+// sit in different banks); a wave whose 256 pixels share one gray value adds them with a single
+// ds_add (flat regions otherwise serialise 64 lanes on one address).  Each block then adds its
+// 256 sums to hist with global atomics: with one block per CU that is 256 atomics per bin.
+// (scripts/exp/hist_variants.hip: one sub-histogram per wave costs 3x on a flat frame; 4096
+// blocks of global atomics, or a last-block reduction over per-block partials, cost 4x.)
+__global__ __launch_bounds__(GH_BS) void k_gray_hist(const uint8_t* __restrict__ bgr, long long N,
+                                                     uint8_t* __restrict__ gray,
+                                                     unsigned* __restrict__ hist) {
+  constexpr int ST = 257, NSUB = GH_BS / 64 * GH_COPIES;
+  __shared__ unsigned sh[NSUB * ST];
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int k = tid; k < NSUB * ST; k += GH_BS) sh[k] = 0;
+  __syncthreads();
+  unsigned* mine = sh + ((tid >> 6) * GH_COPIES + (lane & (GH_COPIES - 1))) * ST;
+  const long long nq = N >> 2;  // full 4-pixel groups
+  const uint32_t* b32 = reinterpret_cast<const uint32_t*>(bgr);
+  const long long stride = (long long)gridDim.x * GH_BS * GH_UNROLL;
+  for (long long q0 = (long long)blockIdx.x * GH_BS * GH_UNROLL + tid; q0 < nq; q0 += stride) {
+    uint32_t w[GH_UNROLL][3];
+#pragma unroll
+    for (int u = 0; u < GH_UNROLL; ++u) {
+      const long long q = q0 + (long long)u * GH_BS;
+      if (q < nq) {
+        w[u][0] = b32[3 * q];
+        w[u][1] = b32[3 * q + 1];
+        w[u][2] = b32[3 * q + 2];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < GH_UNROLL; ++u) {
+      const long long q = q0 + (long long)u * GH_BS;
+      if (q >= nq) break;
+      // B0 G0 R0 B1 | G1 R1 B2 G2 | R2 B3 G3 R3
+      const uint32_t w0 = w[u][0], w1 = w[u][1], w2 = w[u][2];
+      const uint32_t y0 = gray_of(w0 & 255u, (w0 >> 8) & 255u, (w0 >> 16) & 255u);
+      const uint32_t y1 = gray_of(w0 >> 24, w1 & 255u, (w1 >> 8) & 255u);
+      const uint32_t y2 = gray_of((w1 >> 16) & 255u, w1 >> 24, w2 & 255u);
+      const uint32_t y3 = gray_of((w2 >> 8) & 255u, (w2 >> 16) & 255u, w2 >> 24);
+      reinterpret_cast<uint32_t*>(gray)[q] = y0 | (y1 << 8) | (y2 << 16) | (y3 << 24);
+      const uint32_t yw = __builtin_amdgcn_readfirstlane(y0);
+      const unsigned nact = (unsigned)__popcll(__ballot(1));
+      if (__all(y0 == yw && y1 == yw && y2 == yw && y3 == yw)) {
+        if (lane == 0) atomicAdd(mine + yw, 4u * nact);
+      } else {
+        atomicAdd(mine + y0, 1u);
+        atomicAdd(mine + y1, 1u);
+        atomicAdd(mine + y2, 1u);
+        atomicAdd(mine + y3, 1u);
+      }
+    }
+  }
+  if (blockIdx.x == 0 && tid < (int)(N & 3)) {  // ragged tail (< 4 pixels)
+    const long long p = (nq << 2) + tid;
+    const uint32_t y = gray_of(bgr[3 * p], bgr[3 * p + 1], bgr[3 * p + 2]);
+    gray[p] = (uint8_t)y;
+    atomicAdd(mine + y, 1u);
+  }
+  __syncthreads();
+  if (tid < 256) {
+    unsigned s = 0;
+#pragma unroll
+    for (int k = 0; k < NSUB; ++k) s += sh[k * ST + tid];
+    if (s) atomicAdd(hist + tid, s);
+  }
+}
+
+struct NcLut {
+  int32_t v[256];  // marker for each brightness (0 = no level's mean / mean band)
+};
+
+__global__ __launch_bounds__(256) void k_nc_markers(const uint8_t* __restrict__ gray, long long N,
+                                                    int32_t* __restrict__ markers, NcLut lut) {
+  __shared__ int32_t sl[256];
+  sl[threadIdx.x] = lut.v[threadIdx.x];
+  __syncthreads();
+  const long long nq = N >> 2;
+  const uint32_t* g32 = reinterpret_cast<const uint32_t*>(gray);
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
+       q += (long long)gridDim.x * blockDim.x) {
+    const uint32_t g = g32[q];
+    int4 m;
+    m.x = sl[g & 255u];
+    m.y = sl[(g >> 8) & 255u];
+    m.z = sl[(g >> 16) & 255u];
+    m.w = sl[g >> 24];
+    reinterpret_cast<int4*>(markers)[q] = m;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (int)(N & 3)) {
+    const long long p = (nq << 2) + threadIdx.x;
+    markers[p] = sl[gray[p]];
+  }
+}
+
+}  // namespace msg

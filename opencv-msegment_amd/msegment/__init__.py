@@ -19,7 +19,39 @@ import numpy as np
 from . import _lib
 from ._lib import MsegError, Stats
 
-__all__ = ["Segmenter", "MsegError", "Stats", "PictureService"]
+__all__ = ["Segmenter", "MsegError", "Stats", "PictureService", "nc_levels", "nc_marker_lut"]
+
+
+def _levels_out(arr, n):
+    return [(int(arr[k].start), int(arr[k].end), int(arr[k].count)) for k in range(n)]
+
+
+def nc_levels(hist, rows, cols, depth, options=0):
+    """Brightness levels of notConnectedMarkers from a 256-bin histogram (host code of the
+    library, PictureService.java:574-722): list of (start, end, count)."""
+    L = _lib.load()
+    h = np.ascontiguousarray(np.asarray(hist, dtype=np.int32).reshape(256))
+    arr = (_lib.BrightLevel * 256)()
+    n = ctypes.c_int(0)
+    rc = L.msg_nc_levels(ctypes.c_void_p(h.ctypes.data), int(rows), int(cols), int(depth),
+                         int(options), arr, 256, ctypes.byref(n))
+    if rc != 0:
+        raise MsegError(rc, "msg_nc_levels failed")
+    return _levels_out(arr, n.value)
+
+
+def nc_marker_lut(levels, options=0):
+    """Brightness -> marker table of ALLOCATE TO LAYERS (PictureService.java:781-828)."""
+    L = _lib.load()
+    n = len(levels)
+    arr = (_lib.BrightLevel * max(n, 1))()
+    for k, (s, e, c) in enumerate(levels):
+        arr[k].start, arr[k].end, arr[k].count = int(s), int(e), int(c)
+    lut = np.zeros(256, dtype=np.int32)
+    rc = L.msg_nc_marker_lut(arr, n, int(options), ctypes.c_void_p(lut.ctypes.data))
+    if rc != 0:
+        raise MsegError(rc, "msg_nc_marker_lut failed")
+    return lut
 
 
 def _vp(a):
@@ -225,6 +257,35 @@ class Segmenter:
             ctypes.c_void_p(palette.data_ptr()) if palette is not None else None, arr(dsts),
             self._stream(stream)))
         return dsts
+
+    # -- NOT_CONNECTED_MARKERS marker stage (PictureService.java:468-842) ------------------
+    def gray_hist_dev(self, bgr, gray, stream=None):
+        """srcGray = BGR2GRAY(bgr) into ``gray`` (uint8 (H, W) tensor) + its 256-bin histogram."""
+        H, W = bgr.shape[:2]
+        hist = np.zeros(256, dtype=np.int32)
+        self._check(self._L.msg_gray_hist_dev(self._h, ctypes.c_void_p(bgr.data_ptr()), H, W,
+                                              ctypes.c_void_p(gray.data_ptr()),
+                                              ctypes.c_void_p(hist.ctypes.data), self._stream(stream)))
+        return hist
+
+    def nc_markers_dev(self, gray, lut, markers, stream=None):
+        H, W = gray.shape
+        lut = np.ascontiguousarray(np.asarray(lut, dtype=np.int32).reshape(256))
+        self._check(self._L.msg_nc_markers_dev(self._h, ctypes.c_void_p(gray.data_ptr()), H, W,
+                                               ctypes.c_void_p(lut.ctypes.data),
+                                               ctypes.c_void_p(markers.data_ptr()), self._stream(stream)))
+        return markers
+
+    def nc_marker_stage_dev(self, bgr, depth, markers, options=0, gray=None, stream=None):
+        """gray + histogram -> levels -> markers (int32 (H, W) tensor); returns the levels."""
+        H, W = bgr.shape[:2]
+        arr = (_lib.BrightLevel * 256)()
+        n = ctypes.c_int(0)
+        self._check(self._L.msg_nc_marker_stage_dev(
+            self._h, ctypes.c_void_p(bgr.data_ptr()), H, W, int(depth), int(options),
+            ctypes.c_void_p(gray.data_ptr()) if gray is not None else None,
+            ctypes.c_void_p(markers.data_ptr()), arr, 256, ctypes.byref(n), self._stream(stream)))
+        return _levels_out(arr, n.value)
 
     def edge_weights_dev(self, bgr, wright, wdown, stream=None):
         H, W = bgr.shape[:2]

@@ -19,6 +19,10 @@ MSG_EHIP = -2
 MSG_ENOMEM = -3
 MSG_ETIMEOUT = -4
 MSG_ESTATE = -5
+MSG_ERANGE = -6
+
+MSG_NC_GISTO_DIAP = 0x1
+MSG_NC_MULTI_OTSU = 0x2
 
 # every symbol include/msegment.h declares (checked by tests/test_abi.py)
 EXPORTS = (
@@ -27,6 +31,8 @@ EXPORTS = (
     "msg_watershed_dev", "msg_colorize_dev", "msg_watershed_colorize_dev", "msg_edge_weights_dev",
     "msg_set_profiling", "msg_get_kernel_profile", "msg_set_diag",
     "msg_set_batch_inflight", "msg_watershed_colorize_batch_dev",
+    "msg_gray_hist_dev", "msg_nc_levels", "msg_nc_marker_lut", "msg_nc_markers_dev",
+    "msg_nc_marker_stage_dev",
 )
 
 
@@ -49,7 +55,13 @@ class KernelProfile(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int64), ("total_ms", ctypes.c_double)]
 
 
-NKERNELS = 10
+class BrightLevel(ctypes.Structure):
+    """msg_bright_level = model/BrightLevel.java {start, end, count}."""
+
+    _fields_ = [("start", ctypes.c_int32), ("end", ctypes.c_int32), ("count", ctypes.c_int32)]
+
+
+NKERNELS = 12
 
 
 def build(arch="gfx950"):
@@ -114,5 +126,17 @@ def load():
     L.msg_set_batch_inflight.restype = i
     L.msg_watershed_colorize_batch_dev.argtypes = [vp, i, vp, vp, vp, vp, vp, i, vp, vp, vp]
     L.msg_watershed_colorize_batch_dev.restype = i
+    L.msg_gray_hist_dev.argtypes = [vp, vp, i, i, vp, vp, vp]
+    L.msg_gray_hist_dev.restype = i
+    L.msg_nc_levels.argtypes = [vp, i, i, i, ctypes.c_uint, ctypes.POINTER(BrightLevel), i,
+                                ctypes.POINTER(i)]
+    L.msg_nc_levels.restype = i
+    L.msg_nc_marker_lut.argtypes = [ctypes.POINTER(BrightLevel), i, ctypes.c_uint, vp]
+    L.msg_nc_marker_lut.restype = i
+    L.msg_nc_markers_dev.argtypes = [vp, vp, i, i, vp, vp, vp]
+    L.msg_nc_markers_dev.restype = i
+    L.msg_nc_marker_stage_dev.argtypes = [vp, vp, i, i, i, ctypes.c_uint, vp, vp,
+                                          ctypes.POINTER(BrightLevel), i, ctypes.POINTER(i), vp]
+    L.msg_nc_marker_stage_dev.restype = i
     _lib = L
     return L

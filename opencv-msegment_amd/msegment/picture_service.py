@@ -6,14 +6,19 @@ Reference: src/main/java/ru/shayhulud/opencvcmsegment/service/PictureService.jav
   * ``watershed(Mat src, Mat markers, Integer depth, boolean colored)``      :908-911
   * ``colorByIndexes(Mat markers, Integer depth, boolean colored)``          :913-936
   * ``bw_result`` = ``cvtColor(dst, COLOR_BGR2GRAY)``                        :376-379
+  * ``notConnectedMarkers(ii, depth, filterMaskSize, options)``             :468-867
+    (the caller that builds the flood's seeds from brightness levels; see not_connected_markers)
 
 Same names, argument meaning and error behaviour: ``watershed`` rewrites ``markers`` in place
 (like ``Imgproc.watershed``) and returns the colourised Mat; a type/size mismatch raises
 ``MsegError`` where OpenCV's CV_Assert would throw ``CvException``.
 """
 import random
+from collections import namedtuple
 
 from .jrandom import JavaRandom
+
+NcResult = namedtuple("NcResult", "dst bw labels levels colored_markers")
 
 
 class PictureService:
@@ -52,3 +57,50 @@ class PictureService:
     def color_by_indexes(self, markers, depth, colored):
         depth = int(depth)
         return self.segmenter.colorize(markers, depth, self._palette(depth, colored))
+
+    def not_connected_markers(self, src, depth, options=(), colored_markers=False):
+        """PictureService.notConnectedMarkers (PictureService.java:468-867) on the GPU.
+
+        ``options``: names of AlgorithmOptions (model/dic/AlgorithmOptions.java).  COLORED,
+        GISTO_DIAP and MULTI_OTSU change the result; NO_SAVE_STEPS / BW_RESULT only concern
+        saving step images, which is not part of this drop-in (every step image is skipped).
+        MEDIAN_BLUR / BILATERIAL (:481-495) raise MsegError(EINVAL): not built yet.
+
+        Same Random draws as the reference: colorByIndexes(markers, n, true) for the
+        "colored_markers_summ" step (:830) draws n colours before the watershed's own
+        colorByIndexes (:834) draws n more when COLORED.  Returns NcResult(dst = the result
+        image, bw = its BGR2GRAY (:839-841), labels = the flooded marker map, levels, and the
+        coloured marker image when ``colored_markers``).
+        """
+        import numpy as np
+        import torch
+
+        from . import MsegError, _lib
+
+        opts = set(options)
+        if opts & {"MEDIAN_BLUR", "BILATERIAL"}:
+            raise MsegError(_lib.MSG_EINVAL, "MEDIAN_BLUR / BILATERIAL pre-filters not supported")
+        flags = (_lib.MSG_NC_GISTO_DIAP if "GISTO_DIAP" in opts else 0) | (
+            _lib.MSG_NC_MULTI_OTSU if "MULTI_OTSU" in opts else 0)
+        colored = "COLORED" in opts
+        src = np.ascontiguousarray(np.asarray(src, dtype=np.uint8))
+        H, W = src.shape[:2]
+        dev = torch.device("cuda", self.segmenter.device)
+        d_src = torch.from_numpy(src).to(dev)
+        markers = torch.empty((H, W), dtype=torch.int32, device=dev)
+        seg = self.segmenter
+        levels = seg.nc_marker_stage_dev(d_src, int(depth), markers, flags)
+        n = len(levels)
+        step_pal = self._palette(n, True)  # :830, drawn whether or not the step is saved
+        cm = None
+        if colored_markers:
+            cm = torch.empty((H, W, 3), dtype=torch.uint8, device=dev)
+            seg.colorize_dev(markers, n, torch.from_numpy(step_pal).to(dev), cm)
+        pal = self._palette(n, colored)
+        dst = torch.empty((H, W, 3), dtype=torch.uint8, device=dev)
+        bw = torch.empty((H, W), dtype=torch.uint8, device=dev)
+        seg.watershed_colorize_dev(d_src, markers, markers, n,
+                                   torch.from_numpy(pal).to(dev) if pal is not None else None, dst, bw)
+        torch.cuda.synchronize(dev)
+        return NcResult(dst.cpu().numpy(), bw.cpu().numpy(), markers.cpu().numpy(), levels,
+                        cm.cpu().numpy() if cm is not None else None)

@@ -1,0 +1,165 @@
+"""GPU parity of the NOT_CONNECTED_MARKERS marker stage (PictureService.java:468-842) and of the
+whole NC pipeline (marker stage -> watershed -> colorByIndexes -> BGR2GRAY) against the CPU
+oracles (oracle/nc_oracle.py, oracle/ws_oracle.py), bit-exact, through the C ABI."""
+import numpy as np
+import pytest
+
+import msegment
+from msegment import _lib, synth
+from msegment.jrandom import JavaRandom
+from oracle import nc_oracle as O
+from oracle import ws_oracle
+
+pytestmark = pytest.mark.gpu
+
+GISTO = _lib.MSG_NC_GISTO_DIAP
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _dev(a):
+    torch = _torch()
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0")
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (1, 3), (3, 5), (7, 1), (97, 131), (256, 256), (1023, 1025)])
+def test_gray_hist_matches_oracle(seg, shape):
+    torch = _torch()
+    rng = np.random.default_rng(shape[0] * 7 + shape[1])
+    img = rng.integers(0, 256, shape + (3,), dtype=np.uint8)
+    g = torch.zeros(shape, dtype=torch.uint8, device="cuda:0")
+    hist = seg.gray_hist_dev(_dev(img), g)
+    torch.cuda.synchronize()
+    want = O.gray(img)
+    assert np.array_equal(g.cpu().numpy(), want)
+    assert np.array_equal(hist, O.hist256(want))
+
+
+def test_gray_hist_uniform_and_mosaic_4096(seg):
+    torch = _torch()
+    # a constant frame (one bin takes every count: worst-case atomic contention) and the
+    # BASELINE config-3 mosaic
+    for img in (np.full((4096, 4096, 3), 77, np.uint8), synth.mosaic_image(4096, 4096, 2, noise=3)):
+        g = torch.empty(img.shape[:2], dtype=torch.uint8, device="cuda:0")
+        hist = seg.gray_hist_dev(_dev(img), g)
+        torch.cuda.synchronize()
+        want = O.gray(img)
+        assert np.array_equal(g.cpu().numpy(), want)
+        assert np.array_equal(hist, O.hist256(want))
+        assert hist.sum() == img.shape[0] * img.shape[1]
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (5, 3), (64, 64), (333, 517)])
+def test_markers_from_table(seg, shape):
+    torch = _torch()
+    rng = np.random.default_rng(shape[1])
+    gray = rng.integers(0, 256, shape, dtype=np.uint8)
+    lut = rng.integers(-3, 40, 256).astype(np.int32)
+    m = torch.full(shape, 12345, dtype=torch.int32, device="cuda:0")
+    seg.nc_markers_dev(_dev(gray), lut, m)
+    torch.cuda.synchronize()
+    assert np.array_equal(m.cpu().numpy(), O.markers(gray, lut))
+
+
+@pytest.mark.parametrize("opts", [0, GISTO])
+@pytest.mark.parametrize("kind,shape,depth", [("mosaic_noise", (256, 256), 4), ("mosaic", (300, 411), 8),
+                                              ("random", (128, 96), 2)])
+def test_marker_stage_matches_oracle(seg, opts, kind, shape, depth):
+    torch = _torch()
+    img, _, _ = synth.frame(kind, shape[0], shape[1], 5)
+    g, h, lv, mk = O.marker_stage(img, depth, gisto_diap=bool(opts))
+    m = torch.empty(shape, dtype=torch.int32, device="cuda:0")
+    gray = torch.empty(shape, dtype=torch.uint8, device="cuda:0")
+    got = seg.nc_marker_stage_dev(_dev(img), depth, m, opts, gray=gray)
+    torch.cuda.synchronize()
+    assert got == lv
+    assert np.array_equal(gray.cpu().numpy(), g)
+    assert np.array_equal(m.cpu().numpy(), mk)
+    # context scratch for gray
+    m2 = torch.empty(shape, dtype=torch.int32, device="cuda:0")
+    assert seg.nc_marker_stage_dev(_dev(img), depth, m2, opts) == lv
+    torch.cuda.synchronize()
+    assert np.array_equal(m2.cpu().numpy(), mk)
+
+
+def test_marker_stage_multi_otsu(seg):
+    torch = _torch()
+    # three flat patches -> three flex levels -> the multi-Otsu override (k = 3)
+    img = np.zeros((64, 96, 3), np.uint8)
+    img[:, :32] = (20, 30, 40)
+    img[:, 32:64] = (90, 100, 110)
+    img[:, 64:] = (200, 210, 220)
+    g, h, lv, mk = O.marker_stage(img, 4, multi_otsu_opt=True)
+    assert len(O.flex_levels(h, 4)) == 3
+    m = torch.empty((64, 96), dtype=torch.int32, device="cuda:0")
+    assert seg.nc_marker_stage_dev(_dev(img), 4, m, _lib.MSG_NC_MULTI_OTSU) == lv
+    torch.cuda.synchronize()
+    assert np.array_equal(m.cpu().numpy(), mk)
+
+
+def test_marker_stage_errors(seg):
+    torch = _torch()
+    img = np.full((8, 8, 3), 255, np.uint8)  # one bin at 255: never emitted -> no level
+    m = torch.empty((8, 8), dtype=torch.int32, device="cuda:0")
+    with pytest.raises(msegment.MsegError) as e:
+        seg.nc_marker_stage_dev(_dev(img), 4, m)
+    assert e.value.code == _lib.MSG_ESTATE
+    buf = torch.empty(8 * 8 * 4 + 16, dtype=torch.uint8, device="cuda:0")
+    with pytest.raises(msegment.MsegError) as e:  # misaligned marker buffer
+        seg.nc_markers_dev(_dev(np.zeros((8, 8), np.uint8)), np.zeros(256, np.int32), buf[4:].view(torch.int32))
+    assert e.value.code == _lib.MSG_EINVAL
+
+
+def _oracle_nc(img, depth, opts, seed):
+    """notConnectedMarkers end to end on the CPU oracles, with the reference's Random draws."""
+    gisto, otsu, colored = "GISTO_DIAP" in opts, "MULTI_OTSU" in opts, "COLORED" in opts
+    g, h, lv, mk = O.marker_stage(img, depth, gisto_diap=gisto, multi_otsu_opt=otsu)
+    n = len(lv)
+    rnd = JavaRandom(seed)
+    draw = lambda: [rnd.next_int(156) + 100 for _ in range(3)]  # noqa: E731
+    step_pal = np.array([draw() for _ in range(n)], np.uint8).reshape(-1, 3)
+    pal = np.array([draw() for _ in range(n)], np.uint8).reshape(-1, 3) if colored else None
+    labels = ws_oracle.watershed(img, mk)
+    dst = ws_oracle.colorize(labels, n, pal)
+    return dst, ws_oracle.bgr2gray(dst), labels, lv, ws_oracle.colorize(mk, n, step_pal)
+
+
+@pytest.mark.parametrize("opts", [("COLORED",), ("COLORED", "GISTO_DIAP"), ()])
+def test_not_connected_markers_pipeline(opts):
+    img, _, _ = synth.frame("mosaic_noise", 192, 160, 11)
+    ps = msegment.PictureService(seed=2024)
+    r = ps.not_connected_markers(img, 4, opts, colored_markers=True)
+    dst, bw, labels, lv, cm = _oracle_nc(img, 4, opts, 2024)
+    assert r.levels == lv
+    assert np.array_equal(r.labels, labels)
+    assert np.array_equal(r.colored_markers, cm)
+    assert np.array_equal(r.dst, dst)
+    assert np.array_equal(r.bw, bw)
+
+
+def test_not_connected_markers_4096_properties(seg):
+    """Config-3 size: the marker stage bit-exact against the (numpy-fast) oracle stage, and the
+    flood's size-independent properties on its output."""
+    torch = _torch()
+    img = synth.mosaic_image(4096, 4096, 2, noise=3)
+    g, h, lv, mk = O.marker_stage(img, 4, gisto_diap=True)
+    d_img = _dev(img)
+    m = torch.empty((4096, 4096), dtype=torch.int32, device="cuda:0")
+    assert seg.nc_marker_stage_dev(d_img, 4, m, GISTO) == lv
+    torch.cuda.synchronize()
+    assert np.array_equal(m.cpu().numpy(), mk)
+    n = len(lv)
+    dst = torch.empty((4096, 4096, 3), dtype=torch.uint8, device="cuda:0")
+    seg.watershed_colorize_dev(d_img, m, m, n, None, dst)
+    torch.cuda.synchronize()
+    lab = m.cpu().numpy()
+    assert (lab[0, :] == -1).all() and (lab[-1, :] == -1).all()
+    assert (lab[:, 0] == -1).all() and (lab[:, -1] == -1).all()
+    inner = lab[1:-1, 1:-1]
+    seeds = mk[1:-1, 1:-1] > 0
+    assert np.array_equal(inner[seeds], mk[1:-1, 1:-1][seeds])  # seeds keep their label
+    assert set(np.unique(inner)) <= set(range(-1, n + 1))

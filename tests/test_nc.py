@@ -1,0 +1,159 @@
+"""NOT_CONNECTED_MARKERS marker stage (PictureService.java:468-842), CPU side.
+
+* known-answer tests for the level logic, derived by hand from PictureService.java:574-640 /
+  :650-722 / :781-828 and model/BrightLevel.java (each case says which lines it walks through);
+* the oracle restatement (oracle/nc_oracle.py) against those answers;
+* the library's host code (nc_levels.cpp through the C ABI: msg_nc_levels, msg_nc_marker_lut --
+  host-only entry points, no GPU needed) against the oracle on random histograms.
+"""
+import numpy as np
+import pytest
+
+import msegment
+from msegment import _lib
+from oracle import nc_oracle as O
+
+GISTO = _lib.MSG_NC_GISTO_DIAP
+OTSU = _lib.MSG_NC_MULTI_OTSU
+
+
+def H(**bins):
+    h = np.zeros(256, dtype=np.int64)
+    for k, v in bins.items():
+        lo, _, hi = k[1:].partition("_")
+        h[int(lo): int(hi or lo) + 1] = v
+    return h
+
+
+# (histogram, depth, expected flex levels)
+KAT_LEVELS = [
+    # two plateaus: a level extends while the running mean stays in [m/2, 3m/2] (:608-626),
+    # closes on an empty bin (:590-598); a level's count adds its first bin twice (:604, :625)
+    (H(b10_19=100, b30=5), 4, [(10, 19, 1100), (30, 30, 10)]),
+    # block size limit 256/depth = 2 (:578, :617-623): closes every 2 bins
+    (H(b50_54=10), 128, [(50, 51, 30), (52, 53, 20), (54, 54, 10)]),
+    # mean jump 10 -> 55 > 15: split (:627-634)
+    (H(b60=10, b61=100), 4, [(60, 60, 20), (61, 61, 100)]),
+    # empty bin 0 followed by a non-empty bin 1: the initial block [hist[0]] = [0] gives
+    # old mean 0, the band [0, 0] excludes the new mean, so an inverted level (1, 0) is emitted
+    (H(b1=10), 4, [(1, 0, 10), (1, 1, 10)]),
+    # the block still open at bin 255 is never emitted (the loop ends without a flush)
+    (H(b10=3, b255=9), 4, [(10, 10, 6)]),
+]
+
+
+@pytest.mark.parametrize("hist,depth,want", KAT_LEVELS)
+def test_oracle_flex_levels_known_answers(hist, depth, want):
+    assert [l.tup() for l in O.flex_levels(hist, depth)] == want
+
+
+@pytest.mark.parametrize("hist,depth,want", KAT_LEVELS)
+def test_library_flex_levels_known_answers(hist, depth, want):
+    assert msegment.nc_levels(hist, 64, 64, depth) == want
+
+
+def test_known_answer_marker_tables():
+    lv = [(10, 19, 1100), (30, 30, 10), (1, 0, 10), (1, 1, 10)]
+    # means (BrightLevel.getMeanLevel): 10 + 9/2 = 14; 30; (1,0): range -1 -> 1 + (-1)/2 = 1; 1
+    want = np.zeros(256, np.int32)
+    want[14], want[30], want[1] = 1, 2, 3
+    assert np.array_equal(O.marker_lut(lv), want)
+    assert np.array_equal(msegment.nc_marker_lut(lv), want)
+    # GISTO_DIAP (getMeanDiap(3)): (10,19) -> [11, 17]; (30,30) -> itself; (1,0) -> itself
+    # (matches nothing); (1,1) -> itself, so brightness 1 goes to the 4th level
+    want = np.zeros(256, np.int32)
+    want[11:18], want[30], want[1] = 1, 2, 4
+    assert np.array_equal(O.marker_lut(lv, True), want)
+    assert np.array_equal(msegment.nc_marker_lut(lv, GISTO), want)
+
+
+def test_known_answer_multi_otsu_single_level():
+    # one flex level -> one threshold t; overrides [(0, t-1)], then last.end = 255 (:698-712)
+    h = H(b10_19=100)
+    assert O.levels(h, 10, 100, 4, multi_otsu_opt=True) == [(0, 255, 1000)]
+    assert msegment.nc_levels(h, 10, 100, 4, OTSU) == [(0, 255, 1000)]
+
+
+def test_errors_where_the_reference_throws():
+    empty = np.zeros(256, np.int64)
+    with pytest.raises(msegment.MsegError) as e:
+        msegment.nc_levels(empty, 4, 4, 4)
+    assert e.value.code == _lib.MSG_ESTATE
+    with pytest.raises(ValueError):
+        O.levels(empty, 4, 4, 4)
+    with pytest.raises(msegment.MsegError) as e:
+        msegment.nc_levels(H(b3=1), 1, 1, 0)  # 256 / 0
+    assert e.value.code == _lib.MSG_EINVAL
+    # 8 separated spikes -> 8 flex levels: otsuPart would enumerate ~C(128, 8) splits
+    many = H(**{"b%d" % (10 * k + 5): 7 for k in range(8)})
+    assert len(O.flex_levels(many, 4)) == 8
+    with pytest.raises(msegment.MsegError) as e:
+        msegment.nc_levels(many, 8, 7, 4, OTSU)
+    assert e.value.code == _lib.MSG_ERANGE
+
+
+def test_float_rounding_of_large_bins():
+    # calcHist's CV_32F output read back with (int): 2^24 + 1 -> 2^24
+    h = H(b100=(1 << 24) + 1, b101=(1 << 24) + 3)
+    assert [l.tup() for l in O.flex_levels(h, 4)] == msegment.nc_levels(h, 1 << 13, 1 << 12, 4)
+    assert O.flex_levels(h, 4)[0].count == (1 << 24) * 2 + (1 << 24) + 4
+
+
+def _random_hist(rng, kind):
+    if kind == "dense":
+        h = rng.integers(0, 5000, 256)
+    elif kind == "sparse":
+        h = rng.integers(0, 5000, 256) * (rng.random(256) < 0.3)
+    elif kind == "smooth":
+        x = np.arange(256)
+        h = (4000 * np.exp(-((x - rng.integers(0, 256)) / rng.integers(5, 80)) ** 2)).astype(np.int64)
+        h += rng.integers(0, 3, 256)
+    else:  # "image": the histogram of a small random mosaic
+        img = rng.integers(0, 256, (8, 8, 3), dtype=np.uint8).repeat(8, 0).repeat(8, 1)
+        h = O.hist256(O.gray(img))
+    return h.astype(np.int64)
+
+
+@pytest.mark.parametrize("kind", ["dense", "sparse", "smooth", "image"])
+def test_library_levels_match_oracle_random(kind):
+    rng = np.random.default_rng(1234 + len(kind))
+    for it in range(150):
+        h = _random_hist(rng, kind)
+        depth = int(rng.choice([1, 2, 3, 4, 5, 7, 8, 16, 64, 255, 256, 300]))
+        try:
+            want = [l.tup() for l in O.flex_levels(h, depth)]
+        except ZeroDivisionError:
+            continue
+        if not want:
+            with pytest.raises(msegment.MsegError):
+                msegment.nc_levels(h, 100, 100, depth)
+            continue
+        got = msegment.nc_levels(h, 100, 100, depth)
+        assert got == want, (kind, it, depth)
+        for opt in (0, GISTO):
+            assert np.array_equal(msegment.nc_marker_lut(got, opt), O.marker_lut(want, bool(opt)))
+
+
+def test_library_multi_otsu_matches_oracle_random():
+    rng = np.random.default_rng(77)
+    seen = set()
+    tries = 0
+    while len(seen) < 3 or tries < 40:
+        tries += 1
+        assert tries < 2000
+        # 1..3 separated plateaus -> k = 1..3 flex levels
+        k = int(rng.integers(1, 4))
+        h = np.zeros(256, np.int64)
+        starts = np.sort(rng.choice(np.arange(2, 250, 12), k, replace=False))
+        for s in starts:
+            h[s: s + int(rng.integers(1, 8))] = int(rng.integers(1, 3000))
+        lv = O.flex_levels(h, 2)
+        if not 1 <= len(lv) <= 3:
+            continue
+        seen.add(len(lv))
+        rows, cols = int(rng.integers(1, 200)), int(rng.integers(1, 200))
+        want = O.levels(h, rows, cols, 2, multi_otsu_opt=True)
+        got = msegment.nc_levels(h, rows, cols, 2, OTSU)
+        assert got == want
+        for opt in (0, GISTO):
+            assert np.array_equal(msegment.nc_marker_lut(got, opt), O.marker_lut(want, bool(opt)))
