@@ -7,6 +7,8 @@ int32 buffer, the input markers stay pristine) + colorByIndexes(colored=false) i
 through libmsegment's device entry point msg_watershed_colorize_dev.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py --pipeline nc [--kind mosaic_noise]   # notConnectedMarkers'
+      marker stage (gray + histogram -> levels -> markers) + watershed + colorByIndexes per step
 
 N > 1 (launched by torch.distributed.run, one rank per GPU): every rank segments its own frame
 (BASELINE config 5: batched frames, one per GPU, no collectives -- weak scaling).  The only
@@ -26,10 +28,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "opencv-msegment_amd"))
 
 METRIC = "Mpixels/sec segmented at 4096x4096 RGB; achieved HBM GB/s vs peak"
+METRIC_NC = "Mpixels/sec segmented by notConnectedMarkers (marker stage + watershed + colorByIndexes)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
 # Algorithmic bytes (DESIGN.md "Kernels"): what each kernel must move at minimum per unit.
-BYTES_PER_PIXEL = {"k_prep": 15.0, "k_untile": 15.0, "k_colorize": 7.0, "k_edge_weights": 5.0}
+BYTES_PER_PIXEL = {"k_prep": 15.0, "k_untile": 15.0, "k_colorize": 7.0, "k_edge_weights": 5.0,
+                   "k_gray_hist": 4.0, "k_nc_markers": 5.0}
 # k_resolve per item: queue entry 4 + own weights 4 + 4 neighbour states 16, out ipx 4 + granule 8
 # + desc 8 (push-competitor reads are data dependent and not counted)
 BYTES_PER_ITEM = {"k_resolve": 44.0}        # per batch item resolved
@@ -121,11 +125,29 @@ def cpu_baseline(img, m, depth, budget_s=12.0, max_reps=10):
                       % (reps, H, W, t_tot)}, lab
 
 
+def cpu_baseline_nc(img, depth_opt, options, budget_s=12.0, max_reps=10):
+    """The oracles of the NC pipeline (numpy marker stage + the C flood), serial, same frame."""
+    from oracle import nc_oracle, ws_oracle
+
+    H, W = img.shape[:2]
+    reps, t_tot = 0, 0.0
+    while reps < max_reps and t_tot < budget_s:
+        t0 = time.perf_counter()
+        _, _, lv, mk = nc_oracle.marker_stage(img, depth_opt, gisto_diap="GISTO_DIAP" in options)
+        lab = ws_oracle.watershed(img, mk)
+        ws_oracle.colorize(lab, len(lv), None)
+        t_tot += time.perf_counter() - t0
+        reps += 1
+    return {"value": round(H * W * reps / t_tot / 1e6, 3), "unit": "Mpx/s", "cores": 1, "kind": "port",
+            "sample": "%d full %dx%d frame(s): oracle/nc_oracle.py marker stage (numpy) + ws_oracle.c "
+                      "watershed + colorize, 1 thread, %.1f s" % (reps, H, W, t_tot)}, lab
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="default 10 (nc: 2)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 3 (nc: 1)")
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--kind", default="mosaic", choices=["mosaic", "mosaic_noise", "random"])
     ap.add_argument("--seed", type=int, default=None, help="default: 2 (N=1), 100+rank (N>1)")
@@ -134,9 +156,18 @@ def main(argv=None):
                          "default 1 = the headline single-frame step")
     ap.add_argument("--inflight", type=int, default=8,
                     help="floods kept in flight together when --frames > 1")
+    ap.add_argument("--pipeline", default="watershed", choices=["watershed", "nc"],
+                    help="nc: notConnectedMarkers' marker stage builds the seeds each step")
+    ap.add_argument("--nc-depth", type=int, default=4, help="user depth of the nc pipeline")
+    ap.add_argument("--nc-options", default="GISTO_DIAP", help="comma list: GISTO_DIAP,MULTI_OTSU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile-pass", action="store_true")
     args = ap.parse_args(argv)
+    # the nc pipeline's scattered seeds put the flood in its slowest regime
+    if args.steps is None:
+        args.steps = 2 if args.pipeline == "nc" else 10
+    if args.warmup is None:
+        args.warmup = 1 if args.pipeline == "nc" else 3
 
     rank, world, local = dist_env()
     import numpy as np
@@ -181,6 +212,21 @@ def main(argv=None):
         seg.watershed_colorize_batch_dev(b_img, b_m, b_lab, depth, None, b_dst)
 
     step = step1 if K == 1 else stepk
+    NC = args.pipeline == "nc"
+    if NC:
+        if K > 1:
+            raise SystemExit("--pipeline nc runs one frame per step")
+        nc_opts = [o for o in args.nc_options.split(",") if o]
+        nc_flags = sum({"GISTO_DIAP": 1, "MULTI_OTSU": 2}[o] for o in nc_opts)
+        t_gray = torch.empty((S, S), dtype=torch.uint8, device=dev)
+        nc_levels = []
+
+        def step1():  # noqa: F811
+            lv = seg.nc_marker_stage_dev(t_img, args.nc_depth, t_lab, nc_flags, gray=t_gray)
+            nc_levels[:] = lv
+            seg.watershed_colorize_dev(t_img, t_lab, t_lab, len(lv), None, t_dst)
+
+        step = step1
 
     for _ in range(args.warmup):
         step()
@@ -189,7 +235,7 @@ def main(argv=None):
     parity = None
     dgs = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
     dkey = "%s_%dx%d_s%d" % (args.kind, S, S, seed)
-    if rank == 0 and dkey in dgs:  # committed oracle digest of this exact frame
+    if rank == 0 and dkey in dgs and not NC:  # committed oracle digest of this exact frame
         got = hashlib.sha256(t_lab.cpu().numpy().tobytes()).hexdigest()
         parity = ("bit-exact vs oracle digest" if got == dgs[dkey]["labels_sha256"]
                   else "MISMATCH vs oracle digest") + " " + dkey
@@ -213,7 +259,7 @@ def main(argv=None):
         kern = kernel_roofline(prof, st if K == 1 else seg.stats(), S * S, args.steps)
 
     pcie = None
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not NC:
         # host-buffer entry point (what the JNI shim calls): H2D + flood + colourise + D2H
         reps, t_host = 3, 0.0
         for _ in range(reps):
@@ -226,7 +272,10 @@ def main(argv=None):
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, cpu_lab = cpu_baseline(img, m, depth)
+        if NC:
+            cpu, cpu_lab = cpu_baseline_nc(img, args.nc_depth, nc_opts)
+        else:
+            cpu, cpu_lab = cpu_baseline(img, m, depth)
         if parity is None:
             parity = "bit-exact vs oracle" if np.array_equal(cpu_lab, t_lab.cpu().numpy()) else "MISMATCH vs oracle"
 
@@ -250,14 +299,17 @@ def main(argv=None):
                     "alg_bytes_per_launch": top["alg_bytes_per_launch"], "avg_launch_us": top["avg_us"]}
         e2e_gbs = value * 1e6 * E2E_BYTES_PER_PIXEL / 1e9
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world,
+            "metric": METRIC_NC if NC else METRIC, "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (msegment.synth %s, splitmix64; regenerated on the box)" % args.kind,
-            "config": {"workload": "%s %dx%d seed %s%s, watershed + colorByIndexes(colored=false), "
+            "config": {"workload": "%s %dx%d seed %s%s, %s + colorByIndexes(colored=false), "
                                    "device-resident (BASELINE config %s)"
                                    % (args.kind, S, S, seed if (world == 1 or args.seed is not None) else "100+rank",
                                       "" if K == 1 else "..+%d, %d floods in flight" % (K - 1, min(K, args.inflight)),
+                                      ("notConnectedMarkers marker stage (depth %d, %s; %d levels) + watershed"
+                                       % (args.nc_depth, "+".join(nc_opts) or "no options", len(nc_levels)))
+                                      if NC else "watershed",
                                       ({1024: "2", 16384: "4 frame on one GPU"}.get(S, "3") if K == 1
                                        else "5 batching") if world == 1 else "5"),
                        "frames_per_rank_per_step": K, "parallelism": "replicas%d (no collectives)" % world},

@@ -191,6 +191,12 @@ int msg_nc_marker_stage_dev(msg_ctx* ctx, const void* d_bgr, int rows, int cols,
                             msg_bright_level* levels, int max_levels, int* n_levels,
                             void* stream);
 
+/* Host-buffer form of the marker stage (synchronous; strides in bytes): bgr in, the int32
+ * marker map out.  For callers without device memory (the JNI shim). */
+int msg_nc_marker_stage(msg_ctx* ctx, const uint8_t* bgr, size_t bgr_stride, int rows, int cols,
+                        int depth, unsigned options, int32_t* markers, size_t marker_stride,
+                        msg_bright_level* levels, int max_levels, int* n_levels);
+
 #ifdef __cplusplus
 }
 #endif

@@ -846,4 +846,28 @@ int msg_nc_marker_stage_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, i
   return MSG_OK;
 }
 
+int msg_nc_marker_stage(msg_ctx* c, const uint8_t* bgr, size_t bgr_stride, int rows, int cols,
+                        int depth, unsigned options, int32_t* markers, size_t marker_stride,
+                        msg_bright_level* levels, int max_levels, int* n_levels) {
+  int rc = host_args(c, bgr, bgr_stride, markers, marker_stride, rows, cols);
+  if (rc) return rc;
+  if (!n_levels || (max_levels > 0 && !levels)) return fail(c, MSG_EINVAL, "null level array");
+  const long long N = (long long)rows * cols;
+  HIPCHK(c, hipSetDevice(c->dev));
+  rc = ensure_stage(c, std::max(N, 1ll));
+  if (rc) return rc;
+  hipStream_t st = c->own;
+  if (N > 0)
+    HIPCHK(c, hipMemcpy2DAsync(c->d_img, (size_t)cols * 3, bgr, bgr_stride, (size_t)cols * 3, rows,
+                               hipMemcpyHostToDevice, st));
+  rc = msg_nc_marker_stage_dev(c, c->d_img, rows, cols, depth, options, c->d_gray, c->d_mk, levels,
+                               max_levels, n_levels, st);
+  if (rc) return rc;
+  if (N > 0)
+    HIPCHK(c, hipMemcpy2DAsync(markers, marker_stride, c->d_mk, (size_t)cols * 4, (size_t)cols * 4,
+                               rows, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  return MSG_OK;
+}
+
 }  // extern "C"

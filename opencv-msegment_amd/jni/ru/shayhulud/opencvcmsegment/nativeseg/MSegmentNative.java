@@ -31,6 +31,42 @@ public final class MSegmentNative {
 
     private static native String lastError(long ctx);
 
+    /** Returns the level count or a negative MSG_E* code; markers and levels (3 ints each) filled. */
+    private static native int ncMarkers(long ctx, byte[] bgr, int rows, int cols, int depth, int options,
+                                        int[] markers, int[] levelsOut);
+
+    /** AlgorithmOptions.GISTO_DIAP / MULTI_OTSU bits of msg_nc_marker_stage (msegment.h). */
+    public static final int NC_GISTO_DIAP = 0x1;
+    public static final int NC_MULTI_OTSU = 0x2;
+
+    /**
+     * Drop-in for the marker stage of PictureService.notConnectedMarkers (PictureService.java:476-828):
+     * returns wshedMarkSumm (CV_32SC1) and fills levelsOut with the BrightLevel list (the caller's
+     * fThresholds; its size is the depth passed on to watershed / colorByIndexes).
+     */
+    public static Mat notConnectedMarkers(Mat src, int depth, int options, java.util.List<int[]> levelsOut) {
+        if (src.type() != CvType.CV_8UC3) {
+            throw new CvException("notConnectedMarkers: src must be CV_8UC3");
+        }
+        int rows = src.rows();
+        int cols = src.cols();
+        byte[] bgr = new byte[rows * cols * 3];
+        int[] mk = new int[rows * cols];
+        int[] lv = new int[3 * 256];
+        src.get(0, 0, bgr);
+        long ctx = CTX.get();
+        int n = ncMarkers(ctx, bgr, rows, cols, depth, options, mk, lv);
+        if (n < 0) {
+            throw new CvException("libmsegment error " + n + ": " + lastError(ctx));
+        }
+        for (int i = 0; i < n; i++) {
+            levelsOut.add(new int[]{lv[3 * i], lv[3 * i + 1], lv[3 * i + 2]});
+        }
+        Mat markers = new Mat(src.size(), CvType.CV_32SC1);
+        markers.put(0, 0, mk);
+        return markers;
+    }
+
     /** Drop-in for PictureService.watershed(src, markers, depth, colored) given its palette. */
     public static Mat watershed(Mat src, Mat markers, int depth, byte[] paletteOrNull) {
         if (src.type() != CvType.CV_8UC3 || markers.type() != CvType.CV_32SC1

@@ -268,6 +268,18 @@ class Segmenter:
                                               ctypes.c_void_p(hist.ctypes.data), self._stream(stream)))
         return hist
 
+    def nc_marker_stage(self, bgr, depth, options=0):
+        """Host-buffer marker stage: uint8 (H, W, 3) BGR -> (int32 (H, W) markers, levels)."""
+        bgr, bstride = _img_view(bgr)
+        H, W = bgr.shape[:2]
+        markers = np.zeros((H, W), dtype=np.int32)
+        arr = (_lib.BrightLevel * 256)()
+        n = ctypes.c_int(0)
+        self._check(self._L.msg_nc_marker_stage(self._h, _vp(bgr), bstride, H, W, int(depth),
+                                                int(options), _vp(markers), max(W, 1) * 4, arr, 256,
+                                                ctypes.byref(n)))
+        return markers, _levels_out(arr, n.value)
+
     def nc_markers_dev(self, gray, lut, markers, stream=None):
         H, W = gray.shape
         lut = np.ascontiguousarray(np.asarray(lut, dtype=np.int32).reshape(256))

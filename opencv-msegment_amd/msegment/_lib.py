@@ -32,7 +32,7 @@ EXPORTS = (
     "msg_set_profiling", "msg_get_kernel_profile", "msg_set_diag",
     "msg_set_batch_inflight", "msg_watershed_colorize_batch_dev",
     "msg_gray_hist_dev", "msg_nc_levels", "msg_nc_marker_lut", "msg_nc_markers_dev",
-    "msg_nc_marker_stage_dev",
+    "msg_nc_marker_stage_dev", "msg_nc_marker_stage",
 )
 
 
@@ -138,5 +138,8 @@ def load():
     L.msg_nc_marker_stage_dev.argtypes = [vp, vp, i, i, i, ctypes.c_uint, vp, vp,
                                           ctypes.POINTER(BrightLevel), i, ctypes.POINTER(i), vp]
     L.msg_nc_marker_stage_dev.restype = i
+    L.msg_nc_marker_stage.argtypes = [vp, vp, sz, i, i, i, ctypes.c_uint, vp, sz,
+                                      ctypes.POINTER(BrightLevel), i, ctypes.POINTER(i)]
+    L.msg_nc_marker_stage.restype = i
     _lib = L
     return L

@@ -163,3 +163,16 @@ def test_not_connected_markers_4096_properties(seg):
     seeds = mk[1:-1, 1:-1] > 0
     assert np.array_equal(inner[seeds], mk[1:-1, 1:-1][seeds])  # seeds keep their label
     assert set(np.unique(inner)) <= set(range(-1, n + 1))
+
+
+def test_host_buffer_marker_stage(seg):
+    """msg_nc_marker_stage (the JNI shim's entry point): host buffers in and out."""
+    img, _, _ = synth.frame("mosaic_noise", 211, 173, 9)
+    for opts in (0, GISTO):
+        g, h, lv, mk = O.marker_stage(img, 3, gisto_diap=bool(opts))
+        markers, got = seg.nc_marker_stage(img, 3, opts)
+        assert got == lv
+        assert np.array_equal(markers, mk)
+    with pytest.raises(msegment.MsegError) as e:
+        seg.nc_marker_stage(np.full((4, 4, 3), 255, np.uint8), 3)
+    assert e.value.code == _lib.MSG_ESTATE
