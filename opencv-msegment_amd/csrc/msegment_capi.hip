@@ -46,9 +46,9 @@ struct msg_ctx {
   uint8_t* d_gray = nullptr;
   uint8_t* d_pal = nullptr;
   size_t pal_cap = 0;
-  // pinned control mirror + events
-  int* h_flags = nullptr;  // [2 slots][4]
-  hipEvent_t ev[2] = {nullptr, nullptr};
+  // host-mapped progress mirror {iteration, done, error, remaining}, written by k_scatter
+  int* h_mir = nullptr;
+  int* d_mir = nullptr;  // its device address
   unsigned epoch = 1;
   int group = 8;
   int res_grid = 0;   // co-resident k_resolve blocks (occupancy x CUs), bounded-spin safety
@@ -213,6 +213,23 @@ int check_size(msg_ctx* c, int rows, int cols) {
   return MSG_OK;
 }
 
+// Spin on the host-mapped progress mirror until iteration `target` has reported.  A stream that
+// drains (or fails) without the report ends the wait with an error instead of spinning forever.
+int wait_progress(msg_ctx* c, hipStream_t st, int target) {
+  for (unsigned spins = 1;; ++spins) {
+    if (__atomic_load_n(&c->h_mir[0], __ATOMIC_ACQUIRE) >= target) return MSG_OK;
+    if ((spins & 4095) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(&c->h_mir[0], __ATOMIC_ACQUIRE) >= target) return MSG_OK;
+        return fail(c, MSG_ESTATE, "stream drained before iteration %d reported", target);
+      }
+      if (q != hipErrorNotReady) return fail(c, MSG_EHIP, "flood stream: %s", hipGetErrorString(q));
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 // The exact flood on device buffers, in the context's tiled workspace, then the row-major label
 // map into d_labels (may alias d_mk_in) fused with the colourisation when d_dst is given.
 int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t* d_labels, int H,
@@ -246,6 +263,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   ws.capp = c->d_capp;
   ws.ctl = c->d_ctl;
   ws.diag = c->diag ? c->d_diag : nullptr;
+  ws.hmir = c->d_mir;
   ws.H = H;
   ws.W = W;
   ws.Wt = (W + 3) / 4;
@@ -265,36 +283,34 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   LAUNCH(c, KID_INIT_SCAN, st, k_init_scan, dim3(1), dim3(1024), 0, ws, nrc, c->epoch);
   LAUNCH(c, KID_COMPACT, st, k_compact, dim3((nrc + 255) / 256), dim3(256), 0, ws, nrc);
   LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
-  LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws);
+  LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, -1);
   HIPCHK(c, hipGetLastError());
 
-  int it = 0, slot = 0, prev = -1;
+  // Host loop: groups of iterations, one group always queued ahead.  Progress comes from the
+  // host-mapped mirror that each iteration's k_scatter writes (no copy kernel, no event wait):
+  // after queueing a group the host spins until the previous group's last iteration reported.
+  __atomic_store_n(&c->h_mir[0], -1, __ATOMIC_RELEASE);
+  int it = 0, prev_end = -1;
   c->group = 4;
   long long syncs = 0;
   for (;;) {
     for (int g = 0; g < c->group; ++g, ++it) {
       LAUNCH(c, KID_RESOLVE, st, k_resolve, dim3(gres), dim3(RBS), 0, ws);
       LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);  // + small batches
-      LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws);
+      LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, it);
     }
     HIPCHK(c, hipGetLastError());
-    static_assert(offsetof(Ctl, error) == offsetof(Ctl, done) + sizeof(int) &&
-                      offsetof(Ctl, remaining) == offsetof(Ctl, done) + 2 * sizeof(int),
-                  "polled control words must be contiguous");
-    HIPCHK(c, hipMemcpyAsync(c->h_flags + 4 * slot, &c->d_ctl->done, 3 * sizeof(int),
-                             hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipEventRecord(c->ev[slot], st));
-    if (prev >= 0) {
-      HIPCHK(c, hipEventSynchronize(c->ev[prev]));
+    if (prev_end >= 0) {
+      rc = wait_progress(c, st, prev_end);
+      if (rc) return rc;
       ++syncs;
-      if (c->h_flags[4 * prev] || c->h_flags[4 * prev + 1]) break;
+      if (c->h_mir[1] || c->h_mir[2]) break;
       // fewer queued items -> fewer batches left: shrink the group so that the iterations
       // enqueued past the end of the flood (no-ops, but each still a launch) stay few
-      const int rem = c->h_flags[4 * prev + 2];
+      const int rem = c->h_mir[3];
       c->group = rem > (1 << 20) ? 8 : rem > (1 << 17) ? 4 : rem > (1 << 14) ? 2 : 1;
     }
-    prev = slot;
-    slot ^= 1;
+    prev_end = it - 1;
   }
   {
     const long long nunits = (long long)((H + 3) / 4) * ws.Wt * 8;
@@ -488,9 +504,9 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
   c->dev = device_ordinal;
   if (hipSetDevice(c->dev) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void**)&c->d_ctl, sizeof(Ctl)) != hipSuccess ||
-      hipHostMalloc((void**)&c->h_flags, 8 * sizeof(int), hipHostMallocDefault) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev[0], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev[1], hipEventDisableTiming) != hipSuccess) {
+      hipHostMalloc((void**)&c->h_mir, 4 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer((void**)&c->d_mir, c->h_mir, 0) != hipSuccess) {
     msg_destroy(c);
     return MSG_EHIP;
   }
@@ -525,9 +541,7 @@ void msg_destroy(msg_ctx* c) {
   dfree(c->d_hist);
   dfree(c->d_gscr);
   if (c->h_hist) (void)hipHostFree(c->h_hist);
-  if (c->h_flags) (void)hipHostFree(c->h_flags);
-  for (auto& e : c->ev)
-    if (e) (void)hipEventDestroy(e);
+  if (c->h_mir) (void)hipHostFree(c->h_mir);
   for (auto& e : c->evpool) (void)hipEventDestroy(e);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;

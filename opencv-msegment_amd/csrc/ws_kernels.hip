@@ -1180,7 +1180,16 @@ __device__ void scatter_chunks(const Ws& ws, const Batch& B, int first, int stri
   }
 }
 
-__global__ __launch_bounds__(1024) void k_scatter(Ws ws) {
+__global__ __launch_bounds__(1024) void k_scatter(Ws ws, int iter) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && ws.hmir) {
+    // progress mirror for the host loop: k_scan of this iteration has finished, so its control
+    // words are final.  System-scope stores into pinned host memory; the iteration number is
+    // released last, so a host that sees it also sees the three words before it.
+    __hip_atomic_store(ws.hmir + 1, ws.ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 2, ws.ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 3, ws.ctl->remaining, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   const Batch B = ws.ctl->cbat;
   if (B.nchunk == 0 || ws.ctl->error) return;
   scatter_chunks(ws, B, blockIdx.x, gridDim.x);

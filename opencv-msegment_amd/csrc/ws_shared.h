@@ -119,6 +119,7 @@ struct Ws {
   unsigned* capp;    // CAP_SLOTS x NQ partial bucket-capacity histograms (k_prep -> k_init_scan)
   Ctl* ctl;
   unsigned long long* diag;  // nullptr = off; else 8 counters (msg_set_diag)
+  int* hmir;         // host-mapped progress mirror {iteration, done, error, remaining} (k_scatter)
   int H, W;
   int Wt;            // tiles per tile row = ceil(W / 4)
   int marg;          // tiled words of margin before mk (mk - 2*marg is the allocation start)
