@@ -143,6 +143,48 @@ def cpu_baseline_nc(img, depth_opt, options, budget_s=12.0, max_reps=10):
                       "watershed + colorize, 1 thread, %.1f s" % (reps, H, W, t_tot)}, lab
 
 
+def colour_distance(seg, t_img, img, S, sync, reps=20, check=True):
+    """The stand-alone colour-distance stencil (msg_edge_weights_dev) on the bench
+    frame: HIP-event-timed launches, 5 algorithmic bytes per pixel (3 in, 2 out); its output is
+    checked against numpy on the same frame."""
+    import numpy as np
+    import torch
+
+    wr = torch.empty((S, S), dtype=torch.uint8, device=t_img.device)
+    wd = torch.empty_like(wr)
+    seg.edge_weights_dev(t_img, wr, wd)
+    sync()
+    ok = None
+    if check:
+        x = img.astype(np.int16)
+        er = np.zeros((S, S), np.uint8)
+        ed = np.zeros((S, S), np.uint8)
+        er[:, :-1] = np.abs(x[:, 1:] - x[:, :-1]).max(axis=2)
+        ed[:-1] = np.abs(x[1:] - x[:-1]).max(axis=2)
+        ok = bool(np.array_equal(wr.cpu().numpy(), er) and np.array_equal(wd.cpu().numpy(), ed))
+    seg.set_profiling(True)
+    seg.kernel_profile(reset=True)
+    for _ in range(reps):
+        seg.edge_weights_dev(t_img, wr, wd)
+    sync()
+    prof = seg.kernel_profile(reset=True)
+    seg.set_profiling(False)
+    launches, total_ms = prof.get("k_edge_weights", (0, 0.0))
+    if not launches:
+        return None
+    avg_us = 1000.0 * total_ms / launches
+    gbs = BYTES_PER_PIXEL["k_edge_weights"] * S * S / (avg_us * 1e-6) / 1e9
+    traffic = None
+    if os.path.exists(PMC_SUMMARY):
+        kk = json.load(open(PMC_SUMMARY)).get("kernels", {}).get("k_edge_weights16")
+        if kk:
+            traffic = round(kk["hbm_bytes_per_launch"])
+    return {"bound": "hbm", "kernel": "k_edge_weights16", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5), "avg_launch_us": round(avg_us, 3),
+            "alg_bytes_per_launch": BYTES_PER_PIXEL["k_edge_weights"] * S * S, "traffic": traffic,
+            "launches": launches, "parity": None if ok is None else ("bit-exact vs numpy" if ok else "MISMATCH")}
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -258,6 +300,10 @@ def main(argv=None):
         seg.set_profiling(False)
         kern = kernel_roofline(prof, st if K == 1 else seg.stats(), S * S, args.steps)
 
+    stencil = None
+    if not NC and K == 1:
+        stencil = colour_distance(seg, t_img, img, S, sync, check=(rank == 0))
+
     pcie = None
     if rank == 0 and world == 1 and not NC:
         # host-buffer entry point (what the JNI shim calls): H2D + flood + colourise + D2H
@@ -314,6 +360,7 @@ def main(argv=None):
                                        else "5 batching") if world == 1 else "5"),
                        "frames_per_rank_per_step": K, "parallelism": "replicas%d (no collectives)" % world},
             "roofline": roof,
+            "colour_distance": stencil,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
             "e2e_hbm": {"achieved": round(e2e_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -648,9 +648,16 @@ int msg_edge_weights_dev(msg_ctx* c, const void* d_bgr, void* d_wright, void* d_
   if (!d_bgr || !d_wright || !d_wdown) return fail(c, MSG_EINVAL, "null device pointer");
   HIPCHK(c, hipSetDevice(c->dev));
   hipStream_t st = stream ? (hipStream_t)stream : c->own;
-  const long long th = (N + 3) / 4;
-  LAUNCH(c, KID_EDGE, st, k_edge_weights, dim3((unsigned)((th + 255) / 256)), dim3(256), 0,
-         (const uint8_t*)d_bgr, (uint8_t*)d_wright, (uint8_t*)d_wdown, rows, cols);
+  const bool vec = cols % 16 == 0 && (((uintptr_t)d_bgr | (uintptr_t)d_wright | (uintptr_t)d_wdown) & 15) == 0;
+  if (vec) {
+    const long long th = (long long)((rows + EW_ROWS - 1) / EW_ROWS) * (cols / 16);
+    LAUNCH(c, KID_EDGE, st, k_edge_weights16, dim3((unsigned)((th + 255) / 256)), dim3(256), 0,
+           (const uint8_t*)d_bgr, (uint8_t*)d_wright, (uint8_t*)d_wdown, rows, cols);
+  } else {
+    const long long th = (N + 3) / 4;
+    LAUNCH(c, KID_EDGE, st, k_edge_weights, dim3((unsigned)((th + 255) / 256)), dim3(256), 0,
+           (const uint8_t*)d_bgr, (uint8_t*)d_wright, (uint8_t*)d_wdown, rows, cols);
+  }
   HIPCHK(c, hipGetLastError());
   return MSG_OK;
 }

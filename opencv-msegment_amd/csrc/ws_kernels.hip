@@ -57,7 +57,74 @@ __device__ __forceinline__ void st_granule(unsigned long long* p, unsigned long 
 
 // ---------------------------------------------------------------------------------------------
 // Stand-alone colour-distance stencil (exposed as msg_edge_weights_dev; the same arithmetic is
-// fused into k_prep).  One thread = 4 consecutive pixels of a row.
+// fused into k_prep): wr[p] = L-inf BGR distance to the right neighbour, wd[p] to the one below,
+// 0 past the edge.  5 algorithmic bytes per pixel (3 in, 2 out).
+//
+// k_edge_weights16: rows whose width is a multiple of 16 (and 16-B aligned buffers): one thread =
+// a 16-pixel column segment of EW_ROWS rows: EW_ROWS + 1 rows of three 16-B loads (the extra row
+// is the next strip's first: 1.25x reads), one dword per row for the right neighbour of pixel
+// 15, one 16-B store per output row.  k_edge_weights: any shape, 4 pixels per thread.
+__device__ __forceinline__ uint32_t byte_of(const uint32_t* w, int i) { return (w[i >> 2] >> (8 * (i & 3))) & 255u; }
+__device__ __forceinline__ uint32_t linf3(const uint32_t* wa, int ia, const uint32_t* wb, int ib) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int x = (int)byte_of(wa, ia + k), y = (int)byte_of(wb, ib + k);
+    m = max(m, (uint32_t)abs(x - y));
+  }
+  return m;
+}
+
+constexpr int EW_ROWS = 4;  // rows per thread of k_edge_weights16: 5 row loads for 4 output rows
+
+__device__ __forceinline__ void ld48(const uint8_t* p, uint32_t* w) {
+  const uint4* a = reinterpret_cast<const uint4*>(p);
+  const uint4 x0 = a[0], x1 = a[1], x2 = a[2];
+  w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
+  w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
+  w[8] = x2.x; w[9] = x2.y; w[10] = x2.z; w[11] = x2.w;
+}
+
+__global__ __launch_bounds__(256) void k_edge_weights16(const uint8_t* __restrict__ img,
+                                                        uint8_t* __restrict__ wr,
+                                                        uint8_t* __restrict__ wd, int H, int W) {
+  const int segs = W >> 4;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int strips = (H + EW_ROWS - 1) / EW_ROWS;
+  if (t >= (long long)strips * segs) return;
+  const int st = (int)(t / segs), sx = (int)(t - (long long)st * segs);
+  const int r0 = st * EW_ROWS;
+  const bool has_r = sx + 1 < segs;
+  // every load of the strip first: EW_ROWS + 1 rows of 48 B, the right neighbours' first dwords
+  uint32_t rows[EW_ROWS + 1][13];
+#pragma unroll
+  for (int i = 0; i <= EW_ROWS; ++i) {
+    const int r = r0 + i;
+    const long long p0 = (long long)r * W + 16ll * sx;
+    if (r < H) {
+      ld48(img + 3 * p0, rows[i]);
+      rows[i][12] = (has_r && i < EW_ROWS) ? *reinterpret_cast<const uint32_t*>(img + 3 * (p0 + 16)) : 0u;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < EW_ROWS; ++i) {
+    const int r = r0 + i;
+    if (r >= H) break;
+    const bool has_d = r + 1 < H;
+    uint32_t orr[4] = {0, 0, 0, 0}, odd[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t vr = (k < 15 || has_r) ? linf3(rows[i], 3 * k, rows[i], 3 * k + 3) : 0u;
+      const uint32_t vd = has_d ? linf3(rows[i], 3 * k, rows[i + 1], 3 * k) : 0u;
+      orr[k >> 2] |= vr << (8 * (k & 3));
+      odd[k >> 2] |= vd << (8 * (k & 3));
+    }
+    const long long p0 = (long long)r * W + 16ll * sx;
+    *reinterpret_cast<uint4*>(wr + p0) = make_uint4(orr[0], orr[1], orr[2], orr[3]);
+    *reinterpret_cast<uint4*>(wd + p0) = make_uint4(odd[0], odd[1], odd[2], odd[3]);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_edge_weights(const uint8_t* __restrict__ img,
                                                       uint8_t* __restrict__ wr,
                                                       uint8_t* __restrict__ wd, int H, int W) {

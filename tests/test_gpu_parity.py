@@ -253,19 +253,22 @@ def test_device_api_torch(seg):
     assert np.array_equal(t_gray.cpu().numpy(), ws_oracle.bgr2gray(col))
 
 
-def test_edge_weights_dev(seg):
+@pytest.mark.parametrize("shape", [(123, 77), (64, 256), (17, 16), (1, 32), (33, 48), (2, 15)])
+def test_edge_weights_dev(seg, shape):
+    """Both stencil kernels: width % 16 == 0 takes the 16-pixel vector path."""
     import torch
 
-    img = synth.random_image(123, 77, 1)
+    H, W = shape
+    img = synth.random_image(H, W, 1 + H)
     dev = torch.device("cuda", seg.device)
     t = torch.from_numpy(img).to(dev)
-    wr = torch.empty((123, 77), dtype=torch.uint8, device=dev)
+    wr = torch.empty((H, W), dtype=torch.uint8, device=dev)
     wd = torch.empty_like(wr)
     seg.edge_weights_dev(t, wr, wd)
     torch.cuda.synchronize()
     x = img.astype(np.int32)
-    er = np.zeros((123, 77), np.uint8)
-    ed = np.zeros((123, 77), np.uint8)
+    er = np.zeros((H, W), np.uint8)
+    ed = np.zeros((H, W), np.uint8)
     er[:, :-1] = np.abs(x[:, 1:] - x[:, :-1]).max(axis=2)
     ed[:-1] = np.abs(x[1:] - x[:-1]).max(axis=2)
     assert np.array_equal(wr.cpu().numpy(), er) and np.array_equal(wd.cpu().numpy(), ed)
