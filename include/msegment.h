@@ -43,7 +43,7 @@ extern "C" {
 #define MSG_ERANGE   (-6)  /* output array too small / search space beyond what the
                               reference could finish (documented per entry point)          */
 
-#define MSG_ABI_VERSION 2
+#define MSG_ABI_VERSION 3
 
 typedef struct msg_ctx msg_ctx;
 
@@ -59,7 +59,7 @@ typedef struct msg_stats {
                                small-batch loop rounds, small-batch loop entries; reserved      */
 } msg_stats;
 
-#define MSG_NKERNELS 12
+#define MSG_NKERNELS 20
 typedef struct msg_kernel_profile {
     char    name[32];       /* kernel name, e.g. "k_resolve"                                   */
     int64_t launches;       /* launches timed since the last reset                              */
@@ -196,6 +196,33 @@ int msg_nc_marker_stage_dev(msg_ctx* ctx, const void* d_bgr, int rows, int cols,
 int msg_nc_marker_stage(msg_ctx* ctx, const uint8_t* bgr, size_t bgr_stride, int rows, int cols,
                         int depth, unsigned options, int32_t* markers, size_t marker_stride,
                         msg_bright_level* levels, int max_levels, int* n_levels);
+
+/* ---- SHAPE_METHOD marker stage: the caller that builds the flood's seeds in
+ * PictureService.shapeAutoMarkerWatershed (PictureService.java:395-466):
+ *   gray (:404-405) -> medianBlur k (:407-408) -> Canny(5, 50) (:415-416)
+ *   -> dilate 3x3, dilate 5x5, subtract (:426-429) -> medianBlur 3 (:435)
+ *   -> connectedComponents(8, CV_32S) = the markers (:441)
+ *   -> depth = findContours(RETR_CCOMP).size() (:447-451; 0 = no contour: the reference
+ *      returns null and never floods).
+ * Then msg_watershed_colorize*(src, markers, depth, ...) is the reference's this.watershed (:455).
+ * ----------------------------------------------------------------------------------------- */
+
+/* Host only: calculateSizeOfSquareBlurMask (:877-899), the median size the stage uses. */
+int msg_blur_mask_size(int rows, int cols);
+
+/* The whole stage on device buffers: d_bgr (rows*cols*3, BGR) in, d_markers (int32 rows*cols)
+ * out; ksize <= 0 picks msg_blur_mask_size (the reference's choice), else the k x k median
+ * (odd, <= 255).  depth / ncomp (host ints): contour count and component count.  d_blur,
+ * d_edges, d_mask (rows*cols bytes each) may be NULL; when given they receive the blurred gray,
+ * the Canny edges and the marker mask (the reference's saved steps :410, :420, :437).  Returns
+ * when depth and ncomp are known (the markers are complete on `stream`). */
+int msg_shape_markers_dev(msg_ctx* ctx, const void* d_bgr, int rows, int cols, int ksize,
+                          void* d_markers, int* depth, int* ncomp, void* d_blur, void* d_edges,
+                          void* d_mask, void* stream);
+
+/* Host-buffer form (synchronous; strides in bytes). */
+int msg_shape_markers(msg_ctx* ctx, const uint8_t* bgr, size_t bgr_stride, int rows, int cols,
+                      int ksize, int32_t* markers, size_t marker_stride, int* depth, int* ncomp);
 
 #ifdef __cplusplus
 }

@@ -21,6 +21,9 @@
 #include "../../include/msegment.h"
 #include "ws_kernels.hip"
 #include "nc_kernels.hip"
+#include "shape_kernels.hip"
+
+#include <hipcub/hipcub.hpp>
 
 using namespace msg;
 
@@ -73,16 +76,27 @@ struct msg_ctx {
   unsigned* h_hist = nullptr;
   uint8_t* d_gscr = nullptr;
   long long gscr_n = 0;
+  // shape marker stage: 6 byte planes, 2 int planes (parents, block keys), 2 block-key arrays,
+  // scan scratch, 4 counters
+  long long sh_n = 0, sh_nb = 0;
+  uint8_t* d_sh8 = nullptr;
+  int* d_sh32 = nullptr;
+  int *d_shF = nullptr, *d_shP = nullptr, *d_shcnt = nullptr;
+  void* d_scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
 };
 
 namespace {
 
 enum KernelId { KID_PREP, KID_INIT_SCAN, KID_COMPACT, KID_RESOLVE, KID_SCAN, KID_SCATTER,
-                KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_GRAY_HIST, KID_NC_MARKERS, KID_SPARE };
+                KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_GRAY_HIST, KID_NC_MARKERS, KID_SPARE,
+                KID_GRAY, KID_MEDIAN, KID_CANNY, KID_CCL, KID_RING, KID_NUMBER, KID_HOLES, KID_SPARE2 };
 const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_compact", "k_resolve",
                                                 "k_scan", "k_scatter", "k_colorize",
                                                 "k_edge_weights", "k_untile", "k_gray_hist",
-                                                "k_nc_markers", "(unused)"};
+                                                "k_nc_markers", "(unused)", "k_gray",
+                                                "k_median", "k_canny_nms", "k_ccl", "k_ring_median3",
+                                                "k_cc_number", "k_holes", "(unused)"};
 
 hipEvent_t pool_event(msg_ctx* c) {
   if (c->evused == c->evpool.size()) {
@@ -486,6 +500,52 @@ int nc_markers(msg_ctx* c, const uint8_t* d_gray, long long N, const int32_t* lu
   return MSG_OK;
 }
 
+int blur_mask_size(int rows, int cols) {  // PictureService.java:877-899
+  const int m = cols <= rows ? cols : rows;
+  if (m < 3) return 1;
+  if (m <= 100) return 5;
+  const double scale = m <= 360 ? 0.025 : m <= 480 ? 0.02 : m <= 720 ? 0.015 : m <= 1080 ? 0.01 : 0.005;
+  const int r = (int)(m * scale);  // Double.intValue()
+  return r % 2 == 0 ? r + 1 : r;
+}
+
+int ensure_shape(msg_ctx* c, long long N, long long nb) {
+  if (c->sh_n >= N && c->sh_nb >= nb) return MSG_OK;
+  dfree(c->d_sh8);
+  dfree(c->d_sh32);
+  dfree(c->d_shF);
+  dfree(c->d_shP);
+  dfree(c->d_scan_tmp);
+  c->d_sh8 = nullptr;
+  c->d_sh32 = nullptr;
+  c->d_shF = c->d_shP = nullptr;
+  c->d_scan_tmp = nullptr;
+  c->sh_n = c->sh_nb = 0;
+  HIPCHK(c, hipMalloc((void**)&c->d_sh8, 6 * N + 64));
+  HIPCHK(c, hipMalloc((void**)&c->d_sh32, 2 * N * sizeof(int) + 64));
+  HIPCHK(c, hipMalloc((void**)&c->d_shF, nb * sizeof(int) + 64));
+  HIPCHK(c, hipMalloc((void**)&c->d_shP, nb * sizeof(int) + 64));
+  if (!c->d_shcnt) HIPCHK(c, hipMalloc((void**)&c->d_shcnt, 4 * sizeof(int)));
+  size_t tb = 0;
+  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, c->d_shF, c->d_shP, (int)nb));
+  HIPCHK(c, hipMalloc(&c->d_scan_tmp, tb + 64));
+  c->scan_tmp_bytes = tb + 64;
+  c->sh_n = N;
+  c->sh_nb = nb;
+  return MSG_OK;
+}
+
+// Union-find labelling of the pixels `mode` selects (k_ccl_*): L = root per pixel, -1 elsewhere.
+int ccl(msg_ctx* c, const uint8_t* a, int* L, int H, int W, int mode, hipStream_t st) {
+  const long long N = (long long)H * W;
+  const int grid = stream_grid(N);
+  LAUNCH(c, KID_CCL, st, k_ccl_init, dim3(grid), dim3(256), 0, a, L, N, mode);
+  LAUNCH(c, KID_CCL, st, k_ccl_merge, dim3(grid), dim3(256), 0, a, L, H, W, mode);
+  LAUNCH(c, KID_CCL, st, k_ccl_compress, dim3(grid), dim3(256), 0, L, N);
+  HIPCHK(c, hipGetLastError());
+  return MSG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -540,6 +600,12 @@ void msg_destroy(msg_ctx* c) {
   dfree(c->d_diag);
   dfree(c->d_hist);
   dfree(c->d_gscr);
+  dfree(c->d_sh8);
+  dfree(c->d_sh32);
+  dfree(c->d_shF);
+  dfree(c->d_shP);
+  dfree(c->d_shcnt);
+  dfree(c->d_scan_tmp);
   if (c->h_hist) (void)hipHostFree(c->h_hist);
   if (c->h_mir) (void)hipHostFree(c->h_mir);
   for (auto& e : c->evpool) (void)hipEventDestroy(e);
@@ -883,6 +949,112 @@ int msg_nc_marker_stage(msg_ctx* c, const uint8_t* bgr, size_t bgr_stride, int r
                                hipMemcpyHostToDevice, st));
   rc = msg_nc_marker_stage_dev(c, c->d_img, rows, cols, depth, options, c->d_gray, c->d_mk, levels,
                                max_levels, n_levels, st);
+  if (rc) return rc;
+  if (N > 0)
+    HIPCHK(c, hipMemcpy2DAsync(markers, marker_stride, c->d_mk, (size_t)cols * 4, (size_t)cols * 4,
+                               rows, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  return MSG_OK;
+}
+
+int msg_blur_mask_size(int rows, int cols) { return blur_mask_size(rows, cols); }
+
+int msg_shape_markers_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, int ksize,
+                          void* d_markers, int* depth, int* ncomp, void* d_blur, void* d_edges,
+                          void* d_mask, void* stream) {
+  if (!c) return MSG_EINVAL;
+  int rc = check_size(c, rows, cols);
+  if (rc) return rc;
+  if (!depth || !ncomp) return fail(c, MSG_EINVAL, "null depth / ncomp pointer");
+  *depth = *ncomp = 0;
+  const long long N = (long long)rows * cols;
+  if (N == 0) return MSG_OK;
+  if (!d_bgr || !d_markers) return fail(c, MSG_EINVAL, "null device pointer");
+  const int k = ksize > 0 ? ksize : blur_mask_size(rows, cols);
+  if (k % 2 == 0 || k > 255) return fail(c, MSG_EINVAL, "median size %d: odd and <= 255", k);
+  HIPCHK(c, hipSetDevice(c->dev));
+  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  const int H = rows, W = cols;
+  const long long nb = (long long)((H + 1) >> 1) * ((W + 1) >> 1);
+  rc = ensure_shape(c, N, nb);
+  if (rc) return rc;
+  uint8_t* gray = c->d_sh8;
+  uint8_t* blur = gray + N;
+  uint8_t* cls = blur + N;
+  uint8_t* edges = cls + N;
+  uint8_t* mask = edges + N;
+  uint8_t* flag = mask + N;
+  int* L = c->d_sh32;
+  int* K = L + N;
+  const int grid = stream_grid(N);
+  LAUNCH(c, KID_GRAY, st, k_gray, dim3(grid), dim3(256), 0, (const uint8_t*)d_bgr, N, gray);
+  const uint8_t* b = gray;
+  if (k > 1) {
+    LAUNCH(c, KID_MEDIAN, st, k_median, dim3((W + MED_BS - 1) / MED_BS, (H + MED_ROWS - 1) / MED_ROWS),
+           dim3(MED_BS), 0, gray, blur, H, W, k);
+    b = blur;
+  }
+  LAUNCH(c, KID_CANNY, st, k_canny_nms, dim3((W + CN_TX - 1) / CN_TX, (H + CN_TY - 1) / CN_TY), dim3(256), 0,
+         b, cls, H, W, 5, 50);  // Canny(brdGray, brdGray, 5, 5 * 10): cvFloor of both thresholds
+  HIPCHK(c, hipGetLastError());
+  // hysteresis: candidates 8-connected to a strong candidate
+  rc = ccl(c, cls, L, H, W, 0, st);
+  if (rc) return rc;
+  HIPCHK(c, hipMemsetAsync(flag, 0, N, st));
+  LAUNCH(c, KID_CCL, st, k_hyst_mark, dim3(grid), dim3(256), 0, cls, L, flag, N);
+  LAUNCH(c, KID_CCL, st, k_hyst_edges, dim3(grid), dim3(256), 0, cls, L, flag, edges, N);
+  LAUNCH(c, KID_RING, st, k_ring_median3, dim3((W + RG_T - 1) / RG_T, (H + RG_T - 1) / RG_T), dim3(256), 0,
+         edges, mask, H, W);
+  HIPCHK(c, hipGetLastError());
+  // markers: 8-connected components of the mask, numbered by their first 2x2 block
+  rc = ccl(c, mask, L, H, W, 1, st);
+  if (rc) return rc;
+  HIPCHK(c, hipMemsetAsync(K, 0x7f, N * sizeof(int), st));
+  HIPCHK(c, hipMemsetAsync(c->d_shF, 0, nb * sizeof(int), st));
+  LAUNCH(c, KID_NUMBER, st, k_cc_minkey, dim3(grid), dim3(256), 0, L, K, N, W);
+  LAUNCH(c, KID_NUMBER, st, k_cc_firstflag, dim3(grid), dim3(256), 0, L, K, c->d_shF, N, W);
+  size_t tb = c->scan_tmp_bytes;
+  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->d_scan_tmp, tb, c->d_shF, c->d_shP, (int)nb, st));
+  LAUNCH(c, KID_NUMBER, st, k_cc_label, dim3(grid), dim3(256), 0, L, K, c->d_shP, (int32_t*)d_markers, N);
+  HIPCHK(c, hipGetLastError());
+  int tailv[2] = {0, 0};
+  HIPCHK(c, hipMemcpyAsync(&tailv[0], c->d_shP + nb - 1, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(&tailv[1], c->d_shF + nb - 1, sizeof(int), hipMemcpyDeviceToHost, st));
+  // holes: background components (4-connected) that do not touch the frame
+  rc = ccl(c, mask, L, H, W, 2, st);
+  if (rc) return rc;
+  HIPCHK(c, hipMemsetAsync(flag, 0, N, st));
+  HIPCHK(c, hipMemsetAsync(c->d_shcnt, 0, sizeof(int), st));
+  LAUNCH(c, KID_HOLES, st, k_hole_border, dim3(std::max(1, (int)std::min<long long>(1024, (2ll * (H + W) + 255) / 256))),
+         dim3(256), 0, L, flag, H, W);
+  LAUNCH(c, KID_HOLES, st, k_hole_count, dim3(grid), dim3(256), 0, L, flag, c->d_shcnt, N);
+  HIPCHK(c, hipGetLastError());
+  int holes = 0;
+  HIPCHK(c, hipMemcpyAsync(&holes, c->d_shcnt, sizeof(int), hipMemcpyDeviceToHost, st));
+  if (d_blur) HIPCHK(c, hipMemcpyAsync(d_blur, b, N, hipMemcpyDeviceToDevice, st));
+  if (d_edges) HIPCHK(c, hipMemcpyAsync(d_edges, edges, N, hipMemcpyDeviceToDevice, st));
+  if (d_mask) HIPCHK(c, hipMemcpyAsync(d_mask, mask, N, hipMemcpyDeviceToDevice, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  if (c->prof) collect_profile(c);
+  *ncomp = tailv[0] + tailv[1];
+  *depth = *ncomp + holes;
+  return MSG_OK;
+}
+
+int msg_shape_markers(msg_ctx* c, const uint8_t* bgr, size_t bgr_stride, int rows, int cols,
+                      int ksize, int32_t* markers, size_t marker_stride, int* depth, int* ncomp) {
+  int rc = host_args(c, bgr, bgr_stride, markers, marker_stride, rows, cols);
+  if (rc) return rc;
+  const long long N = (long long)rows * cols;
+  HIPCHK(c, hipSetDevice(c->dev));
+  rc = ensure_stage(c, std::max(N, 1ll));
+  if (rc) return rc;
+  hipStream_t st = c->own;
+  if (N > 0)
+    HIPCHK(c, hipMemcpy2DAsync(c->d_img, (size_t)cols * 3, bgr, bgr_stride, (size_t)cols * 3, rows,
+                               hipMemcpyHostToDevice, st));
+  rc = msg_shape_markers_dev(c, c->d_img, rows, cols, ksize, c->d_mk, depth, ncomp, nullptr, nullptr,
+                             nullptr, st);
   if (rc) return rc;
   if (N > 0)
     HIPCHK(c, hipMemcpy2DAsync(markers, marker_stride, c->d_mk, (size_t)cols * 4, (size_t)cols * 4,

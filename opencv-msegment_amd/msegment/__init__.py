@@ -299,6 +299,29 @@ class Segmenter:
             ctypes.c_void_p(markers.data_ptr()), arr, 256, ctypes.byref(n), self._stream(stream)))
         return _levels_out(arr, n.value)
 
+    def shape_markers(self, bgr, ksize=None):
+        """Host-buffer SHAPE_METHOD marker stage (PictureService.java:402-452): uint8 (H, W, 3)
+        BGR -> (int32 (H, W) markers, depth = contour count, component count)."""
+        bgr, bstride = _img_view(bgr)
+        H, W = bgr.shape[:2]
+        markers = np.zeros((H, W), dtype=np.int32)
+        depth, ncomp = ctypes.c_int(0), ctypes.c_int(0)
+        self._check(self._L.msg_shape_markers(self._h, _vp(bgr), bstride, H, W, int(ksize or 0),
+                                              _vp(markers), max(W, 1) * 4, ctypes.byref(depth),
+                                              ctypes.byref(ncomp)))
+        return markers, depth.value, ncomp.value
+
+    def shape_markers_dev(self, bgr, markers, ksize=None, blur=None, edges=None, mask=None, stream=None):
+        """Device form: markers (int32 (H, W) tensor) out; optional uint8 (H, W) tensors receive the
+        blurred gray, the Canny edges and the marker mask.  Returns (depth, ncomp)."""
+        H, W = bgr.shape[:2]
+        depth, ncomp = ctypes.c_int(0), ctypes.c_int(0)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        self._check(self._L.msg_shape_markers_dev(self._h, ptr(bgr), H, W, int(ksize or 0), ptr(markers),
+                                                  ctypes.byref(depth), ctypes.byref(ncomp), ptr(blur),
+                                                  ptr(edges), ptr(mask), self._stream(stream)))
+        return depth.value, ncomp.value
+
     def edge_weights_dev(self, bgr, wright, wdown, stream=None):
         H, W = bgr.shape[:2]
         self._check(self._L.msg_edge_weights_dev(self._h, ctypes.c_void_p(bgr.data_ptr()),

@@ -33,6 +33,7 @@ EXPORTS = (
     "msg_set_batch_inflight", "msg_watershed_colorize_batch_dev",
     "msg_gray_hist_dev", "msg_nc_levels", "msg_nc_marker_lut", "msg_nc_markers_dev",
     "msg_nc_marker_stage_dev", "msg_nc_marker_stage",
+    "msg_blur_mask_size", "msg_shape_markers_dev", "msg_shape_markers",
 )
 
 
@@ -141,5 +142,12 @@ def load():
     L.msg_nc_marker_stage.argtypes = [vp, vp, sz, i, i, i, ctypes.c_uint, vp, sz,
                                       ctypes.POINTER(BrightLevel), i, ctypes.POINTER(i)]
     L.msg_nc_marker_stage.restype = i
+    L.msg_blur_mask_size.argtypes = [i, i]
+    L.msg_blur_mask_size.restype = i
+    L.msg_shape_markers_dev.argtypes = [vp, vp, i, i, i, vp, ctypes.POINTER(i), ctypes.POINTER(i),
+                                        vp, vp, vp, vp]
+    L.msg_shape_markers_dev.restype = i
+    L.msg_shape_markers.argtypes = [vp, vp, sz, i, i, i, vp, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
+    L.msg_shape_markers.restype = i
     _lib = L
     return L

@@ -8,6 +8,8 @@ Reference: src/main/java/ru/shayhulud/opencvcmsegment/service/PictureService.jav
   * ``bw_result`` = ``cvtColor(dst, COLOR_BGR2GRAY)``                        :376-379
   * ``notConnectedMarkers(ii, depth, filterMaskSize, options)``             :468-867
     (the caller that builds the flood's seeds from brightness levels; see not_connected_markers)
+  * ``shapeAutoMarkerWatershed(ii, options)``                                :395-466
+    (seeds from Canny edge rings; see shape_auto_marker_watershed)
 
 Same names, argument meaning and error behaviour: ``watershed`` rewrites ``markers`` in place
 (like ``Imgproc.watershed``) and returns the colourised Mat; a type/size mismatch raises
@@ -19,6 +21,7 @@ from collections import namedtuple
 from .jrandom import JavaRandom
 
 NcResult = namedtuple("NcResult", "dst bw labels levels colored_markers")
+ShapeResult = namedtuple("ShapeResult", "dst bw labels depth")
 
 
 class PictureService:
@@ -104,3 +107,34 @@ class PictureService:
         torch.cuda.synchronize(dev)
         return NcResult(dst.cpu().numpy(), bw.cpu().numpy(), markers.cpu().numpy(), levels,
                         cm.cpu().numpy() if cm is not None else None)
+
+    def shape_auto_marker_watershed(self, src, options=()):
+        """PictureService.shapeAutoMarkerWatershed (PictureService.java:395-466) on the GPU.
+
+        gray -> medianBlur(calculateSizeOfSquareBlurMask) -> Canny(5, 50) -> dilate 3 / dilate 5
+        / subtract -> medianBlur 3 -> connectedComponents(8) = markers; depth = the RETR_CCOMP
+        contour count (:447-451) -- ``None`` when there is no contour, like the reference's
+        ``return null``.  Then this.watershed(src, markers, depth, colored) (:455) and the
+        bw_result (:460-462).  ``options``: COLORED changes the result; the save-step options do
+        not apply here.  Returns ShapeResult(dst, bw, labels = the flooded markers, depth).
+        """
+        import numpy as np
+        import torch
+
+        colored = "COLORED" in set(options)
+        src = np.ascontiguousarray(np.asarray(src, dtype=np.uint8))
+        H, W = src.shape[:2]
+        dev = torch.device("cuda", self.segmenter.device)
+        d_src = torch.from_numpy(src).to(dev)
+        markers = torch.empty((H, W), dtype=torch.int32, device=dev)
+        seg = self.segmenter
+        depth, _ = seg.shape_markers_dev(d_src, markers)
+        if depth == 0:
+            return None
+        pal = self._palette(depth, colored)
+        dst = torch.empty((H, W, 3), dtype=torch.uint8, device=dev)
+        bw = torch.empty((H, W), dtype=torch.uint8, device=dev)
+        seg.watershed_colorize_dev(d_src, markers, markers, depth,
+                                   torch.from_numpy(pal).to(dev) if pal is not None else None, dst, bw)
+        torch.cuda.synchronize(dev)
+        return ShapeResult(dst.cpu().numpy(), bw.cpu().numpy(), markers.cpu().numpy(), depth)
