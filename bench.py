@@ -29,11 +29,14 @@ sys.path.insert(0, os.path.join(ROOT, "opencv-msegment_amd"))
 
 METRIC = "Mpixels/sec segmented at 4096x4096 RGB; achieved HBM GB/s vs peak"
 METRIC_NC = "Mpixels/sec segmented by notConnectedMarkers (marker stage + watershed + colorByIndexes)"
+METRIC_SHAPE = "Mpixels/sec segmented by shapeAutoMarkerWatershed (marker stage + watershed + colorByIndexes)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
 # Algorithmic bytes (DESIGN.md "Kernels"): what each kernel must move at minimum per unit.
 BYTES_PER_PIXEL = {"k_prep": 15.0, "k_untile": 15.0, "k_colorize": 7.0, "k_edge_weights": 5.0,
-                   "k_gray_hist": 4.0, "k_nc_markers": 5.0}
+                   "k_gray_hist": 4.0, "k_nc_markers": 5.0,
+                   # shape marker stage: 1 B in + 1 B out per pixel for the 8-bit stencils
+                   "k_gray": 4.0, "k_median": 2.0, "k_canny_nms": 2.0, "k_ring_median3": 2.0}
 # k_resolve per item: queue entry 4 + own weights 4 + 4 neighbour states 16, out ipx 4 + granule 8
 # + desc 8 (push-competitor reads are data dependent and not counted)
 BYTES_PER_ITEM = {"k_resolve": 44.0}        # per batch item resolved
@@ -143,6 +146,30 @@ def cpu_baseline_nc(img, depth_opt, options, budget_s=12.0, max_reps=10):
                       "watershed + colorize, 1 thread, %.1f s" % (reps, H, W, t_tot)}, lab
 
 
+def cpu_baseline_shape(img, budget_s=12.0, max_reps=10, rows=512):
+    """The oracles of the shape pipeline (numpy/scipy marker stage + the C flood) on a band of the
+    frame (the first `rows` rows, the full frame's median size), bounded to ~budget_s."""
+    import numpy as np
+
+    from oracle import shape_oracle, ws_oracle
+
+    k = shape_oracle.blur_mask_size(*img.shape[:2])
+    img = np.ascontiguousarray(img[:rows])
+    H, W = img.shape[:2]
+    reps, t_tot = 0, 0.0
+    while reps < max_reps and t_tot < budget_s:
+        t0 = time.perf_counter()
+        mk, depth = shape_oracle.shape_markers(img, k)
+        lab = ws_oracle.watershed(img, mk)
+        ws_oracle.colorize(lab, depth, None)
+        t_tot += time.perf_counter() - t0
+        reps += 1
+    return {"value": round(H * W * reps / t_tot / 1e6, 3), "unit": "Mpx/s", "cores": 1, "kind": "port",
+            "sample": "%d band(s) of %dx%d (median %d as for the full frame): oracle/shape_oracle.py "
+                      "marker stage (numpy/scipy) + ws_oracle.c watershed + colorize, 1 thread, %.1f s"
+                      % (reps, H, W, k, t_tot)}, None
+
+
 def colour_distance(seg, t_img, img, S, sync, reps=20, check=True):
     """The stand-alone colour-distance stencil (msg_edge_weights_dev) on the bench
     frame: HIP-event-timed launches, 5 algorithmic bytes per pixel (3 in, 2 out); its output is
@@ -198,8 +225,9 @@ def main(argv=None):
                          "default 1 = the headline single-frame step")
     ap.add_argument("--inflight", type=int, default=8,
                     help="floods kept in flight together when --frames > 1")
-    ap.add_argument("--pipeline", default="watershed", choices=["watershed", "nc"],
-                    help="nc: notConnectedMarkers' marker stage builds the seeds each step")
+    ap.add_argument("--pipeline", default="watershed", choices=["watershed", "nc", "shape"],
+                    help="nc: notConnectedMarkers' marker stage builds the seeds each step; "
+                         "shape: shapeAutoMarkerWatershed's (median, Canny, rings, components)")
     ap.add_argument("--nc-depth", type=int, default=4, help="user depth of the nc pipeline")
     ap.add_argument("--nc-options", default="GISTO_DIAP", help="comma list: GISTO_DIAP,MULTI_OTSU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -269,6 +297,18 @@ def main(argv=None):
             seg.watershed_colorize_dev(t_img, t_lab, t_lab, len(lv), None, t_dst)
 
         step = step1
+    SHAPE = args.pipeline == "shape"
+    if SHAPE:
+        if K > 1:
+            raise SystemExit("--pipeline shape runs one frame per step")
+        shape_depth = []
+
+        def step1():  # noqa: F811
+            d, _ = seg.shape_markers_dev(t_img, t_lab)
+            shape_depth[:] = [d]
+            seg.watershed_colorize_dev(t_img, t_lab, t_lab, d, None, t_dst)
+
+        step = step1
 
     for _ in range(args.warmup):
         step()
@@ -277,7 +317,7 @@ def main(argv=None):
     parity = None
     dgs = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
     dkey = "%s_%dx%d_s%d" % (args.kind, S, S, seed)
-    if rank == 0 and dkey in dgs and not NC:  # committed oracle digest of this exact frame
+    if rank == 0 and dkey in dgs and not NC and not SHAPE:  # committed oracle digest of this frame
         got = hashlib.sha256(t_lab.cpu().numpy().tobytes()).hexdigest()
         parity = ("bit-exact vs oracle digest" if got == dgs[dkey]["labels_sha256"]
                   else "MISMATCH vs oracle digest") + " " + dkey
@@ -301,11 +341,11 @@ def main(argv=None):
         kern = kernel_roofline(prof, st if K == 1 else seg.stats(), S * S, args.steps)
 
     stencil = None
-    if not NC and K == 1:
+    if not NC and not SHAPE and K == 1:
         stencil = colour_distance(seg, t_img, img, S, sync, check=(rank == 0))
 
     pcie = None
-    if rank == 0 and world == 1 and not NC:
+    if rank == 0 and world == 1 and not NC and not SHAPE:
         # host-buffer entry point (what the JNI shim calls): H2D + flood + colourise + D2H
         reps, t_host = 3, 0.0
         for _ in range(reps):
@@ -318,15 +358,18 @@ def main(argv=None):
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if NC:
+        if SHAPE:
+            cpu, cpu_lab = cpu_baseline_shape(img)
+        elif NC:
             cpu, cpu_lab = cpu_baseline_nc(img, args.nc_depth, nc_opts)
         else:
             cpu, cpu_lab = cpu_baseline(img, m, depth)
-        if parity is None:
+        if parity is None and cpu_lab is not None:
             parity = "bit-exact vs oracle" if np.array_equal(cpu_lab, t_lab.cpu().numpy()) else "MISMATCH vs oracle"
 
     if world > 1:
         barrier()
+    seg_blur_k = msegment._lib.load().msg_blur_mask_size(S, S) if SHAPE else None
     if rank == 0:
         roof = None
         if kern:
@@ -345,7 +388,7 @@ def main(argv=None):
                     "alg_bytes_per_launch": top["alg_bytes_per_launch"], "avg_launch_us": top["avg_us"]}
         e2e_gbs = value * 1e6 * E2E_BYTES_PER_PIXEL / 1e9
         out = {
-            "metric": METRIC_NC if NC else METRIC, "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world,
+            "metric": METRIC_SHAPE if SHAPE else METRIC_NC if NC else METRIC, "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (msegment.synth %s, splitmix64; regenerated on the box)" % args.kind,
@@ -355,7 +398,9 @@ def main(argv=None):
                                       "" if K == 1 else "..+%d, %d floods in flight" % (K - 1, min(K, args.inflight)),
                                       ("notConnectedMarkers marker stage (depth %d, %s; %d levels) + watershed"
                                        % (args.nc_depth, "+".join(nc_opts) or "no options", len(nc_levels)))
-                                      if NC else "watershed",
+                                      if NC else ("shapeAutoMarkerWatershed marker stage (median %d, depth %d) "
+                                                  "+ watershed" % (seg_blur_k, shape_depth[0])) if SHAPE
+                                      else "watershed",
                                       ({1024: "2", 16384: "4 frame on one GPU"}.get(S, "3") if K == 1
                                        else "5 batching") if world == 1 else "5"),
                        "frames_per_rank_per_step": K, "parallelism": "replicas%d (no collectives)" % world},

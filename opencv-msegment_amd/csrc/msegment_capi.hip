@@ -295,7 +295,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   const int nrc = H * ws.nseg;  // raster chunks
   LAUNCH(c, KID_PREP, st, k_prep, dim3((H + 3) / 4 * ws.nseg), dim3(RSEG), 0, ws, d_mk_in);
   LAUNCH(c, KID_INIT_SCAN, st, k_init_scan, dim3(1), dim3(1024), 0, ws, nrc, c->epoch);
-  LAUNCH(c, KID_COMPACT, st, k_compact, dim3((nrc + 255) / 256), dim3(256), 0, ws, nrc);
+  LAUNCH(c, KID_COMPACT, st, k_compact, dim3((nrc + 3) / 4), dim3(256), 0, ws, nrc);
   LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
   LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, -1);
   HIPCHK(c, hipGetLastError());
@@ -539,8 +539,10 @@ int ensure_shape(msg_ctx* c, long long N, long long nb) {
 int ccl(msg_ctx* c, const uint8_t* a, int* L, int H, int W, int mode, hipStream_t st) {
   const long long N = (long long)H * W;
   const int grid = stream_grid(N);
-  LAUNCH(c, KID_CCL, st, k_ccl_init, dim3(grid), dim3(256), 0, a, L, N, mode);
-  LAUNCH(c, KID_CCL, st, k_ccl_merge, dim3(grid), dim3(256), 0, a, L, H, W, mode);
+  LAUNCH(c, KID_CCL, st, k_ccl_local, dim3((W + CT - 1) / CT, (H + CT - 1) / CT), dim3(256), 0, a, L, H, W,
+         mode);
+  LAUNCH(c, KID_CCL, st, k_ccl_boundary, dim3((W + CT - 1) / CT, (H + CT - 1) / CT), dim3(128), 0, a, L, H, W,
+         mode);
   LAUNCH(c, KID_CCL, st, k_ccl_compress, dim3(grid), dim3(256), 0, L, N);
   HIPCHK(c, hipGetLastError());
   return MSG_OK;
@@ -1011,7 +1013,7 @@ int msg_shape_markers_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, int
   if (rc) return rc;
   HIPCHK(c, hipMemsetAsync(K, 0x7f, N * sizeof(int), st));
   HIPCHK(c, hipMemsetAsync(c->d_shF, 0, nb * sizeof(int), st));
-  LAUNCH(c, KID_NUMBER, st, k_cc_minkey, dim3(grid), dim3(256), 0, L, K, N, W);
+  LAUNCH(c, KID_NUMBER, st, k_cc_minkey, dim3((W + 255) / 256, H), dim3(256), 0, L, K, H, W);
   LAUNCH(c, KID_NUMBER, st, k_cc_firstflag, dim3(grid), dim3(256), 0, L, K, c->d_shF, N, W);
   size_t tb = c->scan_tmp_bytes;
   HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->d_scan_tmp, tb, c->d_shF, c->d_shP, (int)nb, st));

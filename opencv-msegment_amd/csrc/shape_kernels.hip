@@ -31,13 +31,17 @@ __global__ __launch_bounds__(256) void k_gray(const uint8_t* __restrict__ bgr, l
 }
 
 // ---- k x k median, BORDER_REPLICATE (medianBlur) ---------------------------------------------
-// Thread = one column x, rows [r0, r0 + MED_ROWS).  Its window histogram lives in LDS as 16-bit
-// counts, two threads' bins per dword (lane pair), updated with no-return ds_add (a decrement is
-// the add of 0xFFFF / 0xFFFF0000: the bin holds the removed sample, so no borrow crosses halves).
-// The median m is tracked with lt = #samples < m: each update adjusts lt, then m moves until
-// lt <= half < lt + hist[m].
+// Block = one wave = 64 columns, rows [r0, r0 + MED_ROWS).  Each thread's window histogram lives
+// in LDS as 16-bit counts, two threads' bins per dword (lane pair), updated with no-return ds_add
+// (a decrement adds 0xFFFF / 0xFFFF0000: the bin holds the removed sample, so no borrow crosses
+// halves).  The median m is tracked with lt = #samples < m: each update adjusts lt, then m moves
+// until lt <= half < lt + hist[m].  The two rows a step needs (leaving, entering) are fetched
+// for the whole wave's column span (64 + k - 1 bytes) one step AHEAD into registers, staged in
+// LDS, and read from there: one global round trip per step, overlapped with the step before.
 constexpr int MED_BS = 64;
 constexpr int MED_ROWS = 128;
+constexpr int MED_SPAN = MED_BS + 256;  // span bytes for k <= 255 (64 + k - 1 <= 318)
+constexpr int MED_Q = (MED_SPAN + MED_BS - 1) / MED_BS;  // bytes fetched per lane per row
 
 __device__ __forceinline__ int med_bin(const unsigned* h, int v, int lane) {
   const unsigned w = h[v * (MED_BS / 2) + (lane >> 1)];
@@ -47,28 +51,49 @@ __device__ __forceinline__ int med_bin(const unsigned* h, int v, int lane) {
 __global__ __launch_bounds__(MED_BS) void k_median(const uint8_t* __restrict__ src,
                                                    uint8_t* __restrict__ dst, int H, int W, int k) {
   __shared__ unsigned hist[256 * (MED_BS / 2)];
+  __shared__ uint8_t rows[2][MED_SPAN];  // [leaving, entering] row of the current step
   const int lane = threadIdx.x;
   const int x = blockIdx.x * MED_BS + lane;
   const int r0 = blockIdx.y * MED_ROWS;
   const int r1 = min(H, r0 + MED_ROWS);
   for (int i = lane; i < 256 * (MED_BS / 2); i += MED_BS) hist[i] = 0;
-  __syncthreads();
   const bool on = x < W;
   const int h = k >> 1, half = (k * k) >> 1;
+  const int xs = blockIdx.x * MED_BS - h, span = MED_BS + 2 * h;
   const unsigned one = (lane & 1) ? 0x10000u : 1u;
   const unsigned minus = (lane & 1) ? 0xffff0000u : 0xffffffffu;
   unsigned* const hcol = hist + (lane >> 1);
-  auto add_row = [&](int r, unsigned inc) {  // the k samples of row r (clamped) in this window
+  auto fetch = [&](int r, uint8_t (&v)[MED_Q]) {  // span bytes of row r (clamped) into registers
     const uint8_t* row = src + (long long)min(max(r, 0), H - 1) * W;
-    for (int j = -h; j <= h; ++j) {
-      const int v = row[min(max(x + j, 0), W - 1)];
-      atomicAdd(&hcol[v * (MED_BS / 2)], inc);
+#pragma unroll
+    for (int q = 0; q < MED_Q; ++q) {
+      const int j = lane + MED_BS * q;
+      v[q] = (j < span) ? row[min(max(xs + j, 0), W - 1)] : 0;
     }
   };
+  auto stage = [&](int slot, const uint8_t (&v)[MED_Q]) {
+#pragma unroll
+    for (int q = 0; q < MED_Q; ++q) {
+      const int j = lane + MED_BS * q;
+      if (j < span) rows[slot][j] = v[q];
+    }
+  };
+  __syncthreads();
+  // initial window: rows r0 - h .. r0 + h, each staged then added
+  uint8_t a[MED_Q], b[MED_Q];
+  fetch(r0 - h, a);
+  for (int r = r0 - h; r <= r0 + h; ++r) {
+    stage(0, a);
+    if (r < r0 + h) fetch(r + 1, a);
+    __syncthreads();
+    if (on) {
+#pragma unroll 8
+      for (int j = 0; j < k; ++j) atomicAdd(&hcol[rows[0][lane + j] * (MED_BS / 2)], one);
+    }
+    __syncthreads();
+  }
   int m = 0, lt = 0;
   if (on) {
-    for (int r = r0 - h; r <= r0 + h; ++r) add_row(r, one);
-    // first median: scan up from 0
     int acc = 0;
     for (;;) {
       const int c = med_bin(hist, m, lane);
@@ -77,33 +102,42 @@ __global__ __launch_bounds__(MED_BS) void k_median(const uint8_t* __restrict__ s
       ++m;
     }
     lt = acc;
+    dst[(long long)r0 * W + x] = (uint8_t)m;
   }
-  for (int r = r0; r < r1; ++r) {
+  if (r0 + 1 < r1) {
+    fetch(r0 - h, a);
+    fetch(r0 + 1 + h, b);
+  }
+  for (int r = r0 + 1; r < r1; ++r) {
+    stage(0, a);
+    stage(1, b);
+    if (r + 1 < r1) {  // next step's rows, in flight while this step runs
+      fetch(r - h, a);
+      fetch(r + 1 + h, b);
+    }
+    __syncthreads();
     if (on) {
-      if (r > r0) {
-        const uint8_t* out_row = src + (long long)min(max(r - 1 - h, 0), H - 1) * W;
-        const uint8_t* in_row = src + (long long)min(r + h, H - 1) * W;
-        for (int j = -h; j <= h; ++j) {
-          const int xc = min(max(x + j, 0), W - 1);
-          const int vo = out_row[xc], vi = in_row[xc];
-          atomicAdd(&hcol[vo * (MED_BS / 2)], minus);
-          atomicAdd(&hcol[vi * (MED_BS / 2)], one);
-          lt += (vi < m) - (vo < m);
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the adds land before the reads below
-        while (lt > half) {
-          --m;
-          lt -= med_bin(hist, m, lane);
-        }
-        for (;;) {
-          const int c = med_bin(hist, m, lane);
-          if (lt + c > half) break;
-          lt += c;
-          ++m;
-        }
+#pragma unroll 8
+      for (int j = 0; j < k; ++j) {
+        const int vo = rows[0][lane + j], vi = rows[1][lane + j];
+        atomicAdd(&hcol[vo * (MED_BS / 2)], minus);
+        atomicAdd(&hcol[vi * (MED_BS / 2)], one);
+        lt += (vi < m) - (vo < m);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the adds land before the reads below
+      while (lt > half) {
+        --m;
+        lt -= med_bin(hist, m, lane);
+      }
+      for (;;) {
+        const int c = med_bin(hist, m, lane);
+        if (lt + c > half) break;
+        lt += c;
+        ++m;
       }
       dst[(long long)r * W + x] = (uint8_t)m;
     }
+    __syncthreads();
   }
 }
 
@@ -210,27 +244,105 @@ __device__ __forceinline__ void ccl_union(int* L, int a, int b) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_ccl_init(const uint8_t* __restrict__ a, int* __restrict__ L,
-                                                  long long N, int mode) {
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += stride)
-    L[p] = ccl_fg(a, p, mode) ? (int)p : -1;
+// Tiled labelling: k_ccl_local labels each 32 x 32 tile in LDS (same union-find, workgroup
+// scope) and writes every pixel's tile-local root as its global parent (the local root is the
+// smallest global index of that tile's part of the component); k_ccl_boundary then unions only
+// the pairs that cross a tile border (pixels in a tile's top row, left or right column), and
+// k_ccl_compress points every pixel at its final root.
+constexpr int CT = 32;
+
+__device__ __forceinline__ int lfind(int* lp, int x) {
+  int y = __hip_atomic_load(lp + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (y != x) {
+    x = y;
+    y = __hip_atomic_load(lp + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  return x;
 }
 
-__global__ __launch_bounds__(256) void k_ccl_merge(const uint8_t* __restrict__ a, int* L, int H, int W,
-                                                   int mode) {
-  const long long N = (long long)H * W;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += stride) {
-    if (!ccl_fg(a, p, mode)) continue;
-    const int r = (int)(p / W), c = (int)(p - (long long)r * W);
-    if (c > 0 && ccl_fg(a, p - 1, mode)) ccl_union(L, (int)p, (int)(p - 1));
+__device__ __forceinline__ void lunion(int* lp, int a, int b) {
+  a = lfind(lp, a);
+  b = lfind(lp, b);
+  while (a != b) {
+    if (a < b) {
+      const int t = a;
+      a = b;
+      b = t;
+    }
+    const int old = atomicMin(lp + a, b);
+    if (old == a) return;
+    a = lfind(lp, old);
+    b = lfind(lp, b);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ccl_local(const uint8_t* __restrict__ a, int* __restrict__ L,
+                                                   int H, int W, int mode) {
+  __shared__ int lp[CT * CT];
+  __shared__ uint8_t fg[CT * CT];
+  const int tid = threadIdx.x;
+  const int x0 = blockIdx.x * CT, y0 = blockIdx.y * CT;
+  for (int i = tid; i < CT * CT; i += 256) {
+    const int r = y0 + i / CT, c = x0 + i % CT;
+    const bool on = r < H && c < W && ccl_fg(a, (long long)r * W + c, mode);
+    fg[i] = on;
+    lp[i] = on ? i : -1;
+  }
+  __syncthreads();
+  for (int i = tid; i < CT * CT; i += 256) {
+    if (!fg[i]) continue;
+    const int r = i / CT, c = i % CT;
+    if (c > 0 && fg[i - 1]) lunion(lp, i, i - 1);
     if (r > 0) {
-      if (ccl_fg(a, p - W, mode)) ccl_union(L, (int)p, (int)(p - W));
+      if (fg[i - CT]) lunion(lp, i, i - CT);
       if (mode != 2) {
-        if (c > 0 && ccl_fg(a, p - W - 1, mode)) ccl_union(L, (int)p, (int)(p - W - 1));
-        if (c + 1 < W && ccl_fg(a, p - W + 1, mode)) ccl_union(L, (int)p, (int)(p - W + 1));
+        if (c > 0 && fg[i - CT - 1]) lunion(lp, i, i - CT - 1);
+        if (c + 1 < CT && fg[i - CT + 1]) lunion(lp, i, i - CT + 1);
       }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < CT * CT; i += 256) {
+    const int r = y0 + i / CT, c = x0 + i % CT;
+    if (r >= H || c >= W) continue;
+    int v = -1;
+    if (fg[i]) {
+      const int root = lfind(lp, i);
+      v = (y0 + root / CT) * W + x0 + root % CT;
+    }
+    L[(long long)r * W + c] = v;
+  }
+}
+
+// One block per tile, one thread per border pixel that has a previous neighbour (left, up-left,
+// up, up-right) in another tile: the 32 pixels of the top row, then the left and the right
+// column below it.
+__global__ __launch_bounds__(128) void k_ccl_boundary(const uint8_t* __restrict__ a, int* L, int H, int W,
+                                                      int mode) {
+  const int t = threadIdx.x;
+  if (t >= 3 * CT - 2) return;
+  const int x0 = blockIdx.x * CT, y0 = blockIdx.y * CT;
+  int r, c;
+  if (t < CT) {
+    r = y0;
+    c = x0 + t;
+  } else if (t < 2 * CT - 1) {
+    r = y0 + 1 + (t - CT);
+    c = x0;
+  } else {
+    r = y0 + 1 + (t - (2 * CT - 1));
+    c = x0 + CT - 1;
+  }
+  if (r >= H || c >= W) return;
+  const long long p = (long long)r * W + c;
+  if (!ccl_fg(a, p, mode)) return;
+  const bool top = r == y0, left = c == x0, right = c == x0 + CT - 1;
+  if (c > 0 && left && ccl_fg(a, p - 1, mode)) ccl_union(L, (int)p, (int)(p - 1));
+  if (r > 0) {
+    if (top && ccl_fg(a, p - W, mode)) ccl_union(L, (int)p, (int)(p - W));
+    if (mode != 2) {
+      if (c > 0 && (top || left) && ccl_fg(a, p - W - 1, mode)) ccl_union(L, (int)p, (int)(p - W - 1));
+      if (c + 1 < W && (top || right) && ccl_fg(a, p - W + 1, mode)) ccl_union(L, (int)p, (int)(p - W + 1));
     }
   }
 }
@@ -324,18 +436,28 @@ __global__ __launch_bounds__(256) void k_ring_median3(const uint8_t* __restrict_
 }
 
 // ---- marker numbering: first 2x2 block of each component, block-raster order ---------------
-__device__ __forceinline__ int block_key(long long p, int W) {
-  const int r = (int)(p / W), c = (int)(p - (long long)(p / W) * W);
-  return (r >> 1) * ((W + 1) >> 1) + (c >> 1);
-}
-
-__global__ __launch_bounds__(256) void k_cc_minkey(const int* __restrict__ L, int* __restrict__ K,
-                                                   long long N, int W) {
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += stride) {
-    const int l = L[p];
-    if (l >= 0) atomicMin(K + l, block_key(p, W));
+// 2-D grid: blockIdx.y = row, x over columns.  Only pixels with no 8-neighbour (of the same
+// component, i.e. any foreground neighbour) in a block of smaller key contribute: the
+// component's first block passes that test, and big components no longer pile every pixel's
+// atomicMin onto their root's word.
+__global__ __launch_bounds__(256) void k_cc_minkey(const int* __restrict__ L, int* __restrict__ K, int H,
+                                                   int W) {
+  const int r = blockIdx.y, c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= W) return;
+  const int l = L[(long long)r * W + c];
+  if (l < 0) return;
+  const int bw = (W + 1) >> 1;
+  const int key = (r >> 1) * bw + (c >> 1);
+  for (int dr = -1; dr <= 1; ++dr) {
+    const int rr = r + dr;
+    if (rr < 0 || rr >= H) continue;
+    for (int dc = -1; dc <= 1; ++dc) {
+      const int cc = c + dc;
+      if ((dr == 0 && dc == 0) || cc < 0 || cc >= W) continue;
+      if ((rr >> 1) * bw + (cc >> 1) < key && L[(long long)rr * W + cc] >= 0) return;
+    }
   }
+  atomicMin(K + l, key);
 }
 
 __global__ __launch_bounds__(256) void k_cc_firstflag(const int* __restrict__ L, const int* __restrict__ K,

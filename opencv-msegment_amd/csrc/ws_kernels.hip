@@ -611,27 +611,21 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
 }
 
 // Ordered compaction of the phase-1 pixels in raster order into ilist/desc + level histograms:
-// a wave takes 64 raster chunks, a lane copies one chunk's list (k_prep's scratch in qbuf).
+// a wave copies one raster chunk's list (k_prep's scratch in qbuf), 64 entries per step.
 __device__ __forceinline__ int ld_state(const Ws& ws, long long t);
 
 __global__ __launch_bounds__(256) void k_compact(Ws ws, int nrc) {
   if (ws.ctl->bat.n == 0 || ws.ctl->bat.mode != 1) return;
   const int lane = lane_id();
-  const int ch0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;  // this wave's 64 raster chunks
-  if (ch0 >= nrc) return;
-  // lane = one raster chunk; all lanes copy their chunks' j-th pixels together
-  const int ch = ch0 + lane;
-  const int myn = (ch < nrc) ? ws.tot[ch] : 0;
-  long long rs = 0, k0 = 0;
-  if (myn > 0) {
-    const int r = ch / ws.nseg, cs = ch % ws.nseg;
-    rs = (long long)r * ws.W + (long long)cs * RSEG;
-    k0 = ws.choff[ch];
-  }
-  int nmax = myn;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o));
-  for (int j = 0; j < nmax; ++j) {  // wave-uniform
+  const int ch = blockIdx.x * 4 + (threadIdx.x >> 6);  // this wave's raster chunk
+  if (ch >= nrc) return;
+  const int myn = ws.tot[ch];
+  if (myn == 0) return;
+  const int r = ch / ws.nseg, cs = ch % ws.nseg;
+  const long long rs = (long long)r * ws.W + (long long)cs * RSEG;
+  const long long k0 = ws.choff[ch];
+  for (int j0 = 0; j0 < myn; j0 += 64) {  // wave-uniform
+    const int j = j0 + lane;
     const bool on = j < myn;
     const long long k = k0 + j;
     long long bin = -1;

@@ -62,7 +62,7 @@ class BrightLevel(ctypes.Structure):
     _fields_ = [("start", ctypes.c_int32), ("end", ctypes.c_int32), ("count", ctypes.c_int32)]
 
 
-NKERNELS = 12
+NKERNELS = 20
 
 
 def build(arch="gfx950"):
