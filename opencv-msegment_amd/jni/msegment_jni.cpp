@@ -80,4 +80,23 @@ JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNativ
   return n;
 }
 
+// shapeAutoMarkerWatershed's marker stage (PictureService.java:402-452): markers out (the
+// connectedComponents labels), returns the RETR_CCOMP contour count (the watershed depth; 0 =
+// no contour, where the reference returns null) or a negative MSG_E* code.
+JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_shapeMarkers(
+    JNIEnv* env, jclass, jlong ctx, jbyteArray bgr, jint rows, jint cols, jintArray markers) {
+  msg_ctx* c = reinterpret_cast<msg_ctx*>(ctx);
+  if (!c) return MSG_EINVAL;
+  int depth = 0, ncomp = 0;
+  jbyte* pb = static_cast<jbyte*>(env->GetPrimitiveArrayCritical(bgr, nullptr));
+  jint* pm = static_cast<jint*>(env->GetPrimitiveArrayCritical(markers, nullptr));
+  int rc = MSG_EINVAL;
+  if (pb && pm)
+    rc = msg_shape_markers(c, reinterpret_cast<const uint8_t*>(pb), (size_t)cols * 3, rows, cols, 0,
+                           reinterpret_cast<int32_t*>(pm), (size_t)cols * 4, &depth, &ncomp);
+  if (pm) env->ReleasePrimitiveArrayCritical(markers, pm, 0);
+  if (pb) env->ReleasePrimitiveArrayCritical(bgr, pb, JNI_ABORT);
+  return rc ? rc : depth;
+}
+
 }  // extern "C"

@@ -67,6 +67,35 @@ public final class MSegmentNative {
         return markers;
     }
 
+    /** Returns the contour count (>= 0) or a negative MSG_E* code; markers filled. */
+    private static native int shapeMarkers(long ctx, byte[] bgr, int rows, int cols, int[] markers);
+
+    /**
+     * Drop-in for the marker stage of PictureService.shapeAutoMarkerWatershed
+     * (PictureService.java:402-452): returns the connectedComponents markers (CV_32SC1) and puts
+     * the RETR_CCOMP contour count (the depth passed to watershed) in depthOut[0]; 0 contours is
+     * where the reference returns null.
+     */
+    public static Mat shapeMarkers(Mat src, int[] depthOut) {
+        if (src.type() != CvType.CV_8UC3) {
+            throw new CvException("shapeMarkers: src must be CV_8UC3");
+        }
+        int rows = src.rows();
+        int cols = src.cols();
+        byte[] bgr = new byte[rows * cols * 3];
+        int[] mk = new int[rows * cols];
+        src.get(0, 0, bgr);
+        long ctx = CTX.get();
+        int d = shapeMarkers(ctx, bgr, rows, cols, mk);
+        if (d < 0) {
+            throw new CvException("libmsegment error " + d + ": " + lastError(ctx));
+        }
+        depthOut[0] = d;
+        Mat markers = new Mat(src.size(), CvType.CV_32SC1);
+        markers.put(0, 0, mk);
+        return markers;
+    }
+
     /** Drop-in for PictureService.watershed(src, markers, depth, colored) given its palette. */
     public static Mat watershed(Mat src, Mat markers, int depth, byte[] paletteOrNull) {
         if (src.type() != CvType.CV_8UC3 || markers.type() != CvType.CV_32SC1
