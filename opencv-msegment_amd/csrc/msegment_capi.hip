@@ -295,7 +295,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   const int nrc = H * ws.nseg;  // raster chunks
   LAUNCH(c, KID_PREP, st, k_prep, dim3((H + 3) / 4 * ws.nseg), dim3(RSEG), 0, ws, d_mk_in);
   LAUNCH(c, KID_INIT_SCAN, st, k_init_scan, dim3(1), dim3(1024), 0, ws, nrc, c->epoch);
-  LAUNCH(c, KID_COMPACT, st, k_compact, dim3((nrc + 3) / 4), dim3(256), 0, ws, nrc);
+  LAUNCH(c, KID_COMPACT, st, k_compact, dim3((nrc + 4 * CPW - 1) / (4 * CPW)), dim3(256), 0, ws, nrc);
   LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
   LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, -1);
   HIPCHK(c, hipGetLastError());

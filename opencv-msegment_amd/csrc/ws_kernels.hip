@@ -611,39 +611,54 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
 }
 
 // Ordered compaction of the phase-1 pixels in raster order into ilist/desc + level histograms:
-// a wave copies one raster chunk's list (k_prep's scratch in qbuf), 64 entries per step.
+// a wave owns CPW raster chunks and copies each non-empty chunk's list (k_prep's scratch in
+// qbuf) 64 entries per step -- dense seeds do not serialise a long list on one lane (one lane
+// per chunk: 430 us for the shape stage's ring seeds at 4096^2), sparse seeds keep the grid
+// small (one wave per chunk: 29 us for the mosaic's, 32 K mostly idle waves).
 __device__ __forceinline__ int ld_state(const Ws& ws, long long t);
+
+constexpr int CPW = 4;  // raster chunks per k_compact wave
 
 __global__ __launch_bounds__(256) void k_compact(Ws ws, int nrc) {
   if (ws.ctl->bat.n == 0 || ws.ctl->bat.mode != 1) return;
   const int lane = lane_id();
-  const int ch = blockIdx.x * 4 + (threadIdx.x >> 6);  // this wave's raster chunk
-  if (ch >= nrc) return;
-  const int myn = ws.tot[ch];
-  if (myn == 0) return;
-  const int r = ch / ws.nseg, cs = ch % ws.nseg;
-  const long long rs = (long long)r * ws.W + (long long)cs * RSEG;
-  const long long k0 = ws.choff[ch];
-  for (int j0 = 0; j0 < myn; j0 += 64) {  // wave-uniform
-    const int j = j0 + lane;
-    const bool on = j < myn;
-    const long long k = k0 + j;
-    long long bin = -1;
-    if (on) {
-      const int t = ws.qbuf[rs + j];
-      const int lv = ld_state(ws, t) & 255;
-      ws.ilist[k] = t;
-      ws.desc[k] = make_desc((unsigned)lv, 1u, 0, 0);
-      bin = (k / CH) * NQ + lv;
-    }
-    // plateau seeds share a level: one atomic per distinct histogram bin of the wave
-    unsigned long long rem = __ballot(on);
-    while (rem) {
-      const int leader = __ffsll((long long)rem) - 1;
-      const long long lb = __shfl(bin, leader);
-      const unsigned long long same = __ballot(on && bin == lb);
-      if (lane == leader) atomicAdd(&ws.cnt[lb], (int)__popcll(same));
-      rem &= ~same;
+  const int ch0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * CPW;  // this wave's raster chunks
+  if (ch0 >= nrc) return;
+  const int myc = ch0 + lane;
+  const int myn = (lane < CPW && myc < nrc) ? ws.tot[myc] : 0;
+  long long mrs = 0, mk0 = 0;
+  if (myn > 0) {
+    const int r = myc / ws.nseg, cs = myc % ws.nseg;
+    mrs = (long long)r * ws.W + (long long)cs * RSEG;
+    mk0 = ws.choff[myc];
+  }
+  unsigned long long todo = __ballot(myn > 0);
+  while (todo) {  // wave-uniform
+    const int src = __ffsll((long long)todo) - 1;
+    todo &= todo - 1;
+    const int n = __shfl(myn, src);
+    const long long rs = __shfl(mrs, src), k0 = __shfl(mk0, src);
+    for (int j0 = 0; j0 < n; j0 += 64) {
+      const int j = j0 + lane;
+      const bool on = j < n;
+      const long long k = k0 + j;
+      long long bin = -1;
+      if (on) {
+        const int t = ws.qbuf[rs + j];
+        const int lv = ld_state(ws, t) & 255;
+        ws.ilist[k] = t;
+        ws.desc[k] = make_desc((unsigned)lv, 1u, 0, 0);
+        bin = (k / CH) * NQ + lv;
+      }
+      // plateau seeds share a level: one atomic per distinct histogram bin of the wave
+      unsigned long long rem = __ballot(on);
+      while (rem) {
+        const int leader = __ffsll((long long)rem) - 1;
+        const long long lb = __shfl(bin, leader);
+        const unsigned long long same = __ballot(on && bin == lb);
+        if (lane == leader) atomicAdd(&ws.cnt[lb], (int)__popcll(same));
+        rem &= ~same;
+      }
     }
   }
 }
