@@ -9,6 +9,10 @@ cannot run here), so every expected output below is produced by
 resource src/main/resources/images/hkp.jpg with PIL (into raw BGR bytes, stored as data) when the
 reference tree is present; the decoded pixels are what the fixture pins, not the JPEG decoder.
 
+album_1500x1500.png is the reference's resource src/main/resources/images/album.jpg decoded by PIL
+and re-encoded losslessly (write_album below): a real 1500x1500 photograph for the shape-method
+pipeline and real-image flood timing (scripts/real_image_probe.py, tests/test_gpu_real.py).
+
 Outputs (numpy .npz, no pickles):
   small_cases.npz  inputs + expected labels + expected colourised/gray outputs, small frames
   digests.json     SHA-256 of the oracle's label maps for larger synthetic frames
@@ -132,8 +136,18 @@ def write_digests(only=None):
         json.dump(digests, f, indent=1, sort_keys=True)
 
 
+def write_album():
+    from PIL import Image
+
+    src = "/root/reference/src/main/resources/images/album.jpg"
+    rgb = np.asarray(Image.open(src).convert("RGB"))
+    Image.fromarray(rgb).save(os.path.join(OUT, "album_1500x1500.png"), optimize=True)
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "--digests-only":  # e.g. --digests-only mosaic_16384x16384_s3
+    if len(sys.argv) > 1 and sys.argv[1] == "--album":
+        write_album()
+    elif len(sys.argv) > 1 and sys.argv[1] == "--digests-only":  # e.g. --digests-only mosaic_16384x16384_s3
         write_digests(set(sys.argv[2:]) or None)
     else:
         main()
