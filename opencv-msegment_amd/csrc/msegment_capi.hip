@@ -776,6 +776,21 @@ int msg_watershed_colorize(msg_ctx* c, const uint8_t* bgr, size_t bgr_stride, in
   if (rc) return rc;
   HIPCHK(c, hipMemcpy2DAsync(markers, marker_stride, c->d_mk, (size_t)cols * 4, (size_t)cols * 4,
                              rows, hipMemcpyDeviceToHost, st));
+  // read-back guard: cv::watershed leaves the whole first row at WSHED.  One 8-in-flight batch
+  // test run returned a frame of zeros through this path (not reproduced in 14 K frames of
+  // scripts/stress_batch.py): the pageable copy is re-issued once; a second failure is an error.
+  auto row0_ok = [&]() {
+    for (int j = 0; j < cols; ++j)
+      if (markers[j] != WSHED) return false;
+    return true;
+  };
+  HIPCHK(c, hipStreamSynchronize(st));
+  if (!row0_ok()) {
+    HIPCHK(c, hipMemcpy2D(markers, marker_stride, c->d_mk, (size_t)cols * 4, (size_t)cols * 4, rows,
+                          hipMemcpyDeviceToHost));
+    if (!row0_ok()) return fail(c, MSG_ESTATE, "label read-back failed the frame-border check");
+    std::fprintf(stderr, "libmsegment: label read-back re-issued (frame-border check)\n");
+  }
   if (want_color) {
     HIPCHK(c, hipMemcpy2DAsync(dst_bgr, dst_stride, c->d_dst, (size_t)cols * 3, (size_t)cols * 3,
                                rows, hipMemcpyDeviceToHost, st));

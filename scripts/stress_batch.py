@@ -9,6 +9,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "opencv-msegment_amd")]
 
 import numpy as np  # noqa: E402
 
+if os.environ.get("STRESS_TORCH"):  # the pytest session's state: torch's HIP runtime, a busy stream
+    import torch  # noqa: F401
+
 import msegment  # noqa: E402
 from msegment import synth  # noqa: E402
 from oracle import ws_oracle  # noqa: E402
@@ -24,6 +27,15 @@ def main():
                           40 + int(rng.integers(0, 200)), 300 + 10 * v + k)[:2] for k in range(7)]
         sets.append((fr, [ws_oracle.watershed(img, m) for img, m in fr]))
     seg = msegment.Segmenter(0)
+    if os.environ.get("STRESS_TORCH"):
+        x = torch.randn(4096, 4096, device="cuda:0")
+        for _ in range(3):
+            x = x @ x
+        torch.cuda.synchronize()
+    exact = os.environ.get("STRESS_EXACT")
+    if exact:  # tests/test_gpu_parity.py::test_batch_api_inflight's frames
+        fr = [synth.frame(("mosaic", "mosaic_noise")[k % 2], 60 + 17 * k, 90 + 5 * k, 200 + k)[:2] for k in range(7)]
+        sets = [(fr, [ws_oracle.watershed(img, m) for img, m in fr])]
     bad = 0
     t0 = time.time()
     for r in range(reps):
