@@ -178,7 +178,7 @@ void free_stage(msg_ctx* c) {
 
 long long tile_margin(int W) { return 16ll * ((W + 3) / 4 + 1); }  // tiled words
 
-int ensure_flood(msg_ctx* c, int H, int W) {
+int ensure_flood(msg_ctx* c, int H, int W, hipStream_t st) {
   const long long N = (long long)H * W;
   // + a margin of one tile row (+ one tile) before and after: k_resolve's speculative
   // radius-2 loads around frame-adjacent pixels may land there (values discarded)
@@ -190,7 +190,10 @@ int ensure_flood(msg_ctx* c, int H, int W) {
   const long long nch = (n + CH - 1) / CH;
   const long long qcap = 4 * n + 16;
   HIPCHK(c, hipMalloc((void**)&c->d_px_base, np * 8));
-  HIPCHK(c, hipMemset(c->d_px_base, 0, np * 8));
+  // stream-ordered: a null-stream hipMemset does not order with the non-blocking flood stream
+  // and could land after k_prep's first writes (seen as an all-zero label map / ERR_STATE on
+  // the first flood of a fresh batch sub-context)
+  HIPCHK(c, hipMemsetAsync(c->d_px_base, 0, np * 8, st));
   HIPCHK(c, hipMalloc((void**)&c->d_ilist, n * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_qbuf, qcap * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_tl, n * 8));
@@ -200,7 +203,7 @@ int ensure_flood(msg_ctx* c, int H, int W) {
   HIPCHK(c, hipMalloc((void**)&c->d_tot, rc * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_choff, rc * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_capp, (size_t)CAP_SLOTS * NQ * 4));
-  HIPCHK(c, hipMemset(c->d_tl, 0, n * 8));
+  HIPCHK(c, hipMemsetAsync(c->d_tl, 0, n * 8, st));
   c->epoch = 1;
   c->cap_n = n;
   c->cap_np = np;
@@ -254,7 +257,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   c->stats.rows = H;
   c->stats.cols = W;
   if (N == 0) return MSG_OK;
-  int rc = ensure_flood(c, H, W);
+  int rc = ensure_flood(c, H, W, st);
   if (rc) return rc;
   if (c->epoch > 0x70000000u) {  // granule bit 63 flags a provisional value
     HIPCHK(c, hipMemsetAsync(c->d_tl, 0, c->cap_n * 8, st));
@@ -776,9 +779,9 @@ int msg_watershed_colorize(msg_ctx* c, const uint8_t* bgr, size_t bgr_stride, in
   if (rc) return rc;
   HIPCHK(c, hipMemcpy2DAsync(markers, marker_stride, c->d_mk, (size_t)cols * 4, (size_t)cols * 4,
                              rows, hipMemcpyDeviceToHost, st));
-  // read-back guard: cv::watershed leaves the whole first row at WSHED.  One 8-in-flight batch
-  // test run returned a frame of zeros through this path (not reproduced in 14 K frames of
-  // scripts/stress_batch.py): the pageable copy is re-issued once; a second failure is an error.
+  // read-back guard: cv::watershed leaves the whole first row at WSHED.  (An all-zero frame was
+  // once returned here: the workspace's zero fill ran as a null-stream hipMemset, unordered with
+  // the flood stream -- fixed in ensure_flood; the check stays as a cheap consistency test.)
   auto row0_ok = [&]() {
     for (int j = 0; j < cols; ++j)
       if (markers[j] != WSHED) return false;
@@ -786,8 +789,9 @@ int msg_watershed_colorize(msg_ctx* c, const uint8_t* bgr, size_t bgr_stride, in
   };
   HIPCHK(c, hipStreamSynchronize(st));
   if (!row0_ok()) {
-    HIPCHK(c, hipMemcpy2D(markers, marker_stride, c->d_mk, (size_t)cols * 4, (size_t)cols * 4, rows,
-                          hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy2DAsync(markers, marker_stride, c->d_mk, (size_t)cols * 4, (size_t)cols * 4, rows,
+                               hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
     if (!row0_ok()) return fail(c, MSG_ESTATE, "label read-back failed the frame-border check");
     std::fprintf(stderr, "libmsegment: label read-back re-issued (frame-border check)\n");
   }
