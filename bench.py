@@ -170,6 +170,37 @@ def cpu_baseline_shape(img, budget_s=12.0, max_reps=10, rows=512):
                       % (reps, H, W, k, t_tot)}, None
 
 
+def batch_throughput(seg, args, S, seed, sync, steps=5, warmup=2):
+    """BASELINE config 5 on this GPU: --batch-frames frames of the same workload per call, up to
+    --inflight floods in flight (msg_watershed_colorize_batch_dev); whole-batch Mpx/s."""
+    import torch
+
+    from msegment import synth
+
+    K = args.batch_frames
+    dev = torch.device("cuda", torch.cuda.current_device())
+    fr = [synth.frame(args.kind, S, S, seed + k) for k in range(K)]
+    depth = max(f[2] for f in fr)
+    imgs = [torch.from_numpy(f[0]).to(dev) for f in fr]
+    mks = [torch.from_numpy(f[1]).to(dev) for f in fr]
+    labs = [torch.empty_like(m) for m in mks]
+    dsts = [torch.empty((S, S, 3), dtype=torch.uint8, device=dev) for _ in fr]
+    seg.set_batch_inflight(args.inflight)
+    for _ in range(warmup):
+        seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)
+    sync()
+    dt = time.perf_counter() - t0
+    del imgs, mks, labs, dsts
+    return {"value": round(K * S * S * steps / dt / 1e6, 3), "unit": "Mpx/s", "frames": K,
+            "inflight": min(K, args.inflight), "steps": steps,
+            "note": "BASELINE config 5 per GPU: %d frames (seeds %d..%d) per call, floods overlapped"
+                    % (K, seed, seed + K - 1)}
+
+
 def colour_distance(seg, t_img, img, S, sync, reps=20, check=True):
     """The stand-alone colour-distance stencil (msg_edge_weights_dev) on the bench
     frame: HIP-event-timed launches, 5 algorithmic bytes per pixel (3 in, 2 out); its output is
@@ -225,6 +256,8 @@ def main(argv=None):
                          "default 1 = the headline single-frame step")
     ap.add_argument("--inflight", type=int, default=8,
                     help="floods kept in flight together when --frames > 1")
+    ap.add_argument("--batch-frames", type=int, default=8,
+                    help="frames of the extra 'batch' measurement (config 5 per GPU); 0/1 = skip")
     ap.add_argument("--pipeline", default="watershed", choices=["watershed", "nc", "shape"],
                     help="nc: notConnectedMarkers' marker stage builds the seeds each step; "
                          "shape: shapeAutoMarkerWatershed's (median, Canny, rings, components)")
@@ -344,6 +377,10 @@ def main(argv=None):
     if not NC and not SHAPE and K == 1:
         stencil = colour_distance(seg, t_img, img, S, sync, check=(rank == 0))
 
+    batch = None
+    if K == 1 and not NC and not SHAPE and args.batch_frames > 1:
+        batch = batch_throughput(seg, args, S, seed, sync)
+
     pcie = None
     if rank == 0 and world == 1 and not NC and not SHAPE:
         # host-buffer entry point (what the JNI shim calls): H2D + flood + colourise + D2H
@@ -406,6 +443,7 @@ def main(argv=None):
                        "frames_per_rank_per_step": K, "parallelism": "replicas%d (no collectives)" % world},
             "roofline": roof,
             "colour_distance": stencil,
+            "batch": batch,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
             "e2e_hbm": {"achieved": round(e2e_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
