@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -384,6 +385,13 @@ int upload_palette(msg_ctx* c, const uint8_t* pal, int depth, hipStream_t st) {
 
 constexpr int MAX_INFLIGHT = 8;
 
+// Hardware queues per process of the HIP runtime (GPU_MAX_HW_QUEUES, default 4).
+int hw_queues() {
+  const char* e = getenv("GPU_MAX_HW_QUEUES");
+  const int q = e ? atoi(e) : 0;
+  return q > 0 ? q : 4;
+}
+
 int ensure_subs(msg_ctx* c, int k) {
   while ((int)c->subs.size() < k) {
     msg_ctx* sub = nullptr;
@@ -421,6 +429,12 @@ int run_batch(msg_ctx* c, int n, F fn) {
   }
   int rc = ensure_subs(c, k);
   if (rc) return rc;
+  // up to min(k, hardware queues) floods run kernels concurrently (streams beyond the HIP
+  // runtime's hardware queues share them and serialise): k_resolve's waits on lower ranks are
+  // only safe while every block of every concurrent k_resolve grid can be resident at once, so
+  // the co-resident budget (occupancy x CUs) is split between the concurrent floods
+  const int conc = std::max(1, std::min(k, hw_queues()));
+  for (int w = 0; w < k; ++w) c->subs[w]->res_grid = std::max(1, c->res_grid / conc);
   std::vector<int> rcs(k, MSG_OK);
   std::vector<msg_stats> st(k);
   std::vector<std::thread> th;

@@ -1,6 +1,6 @@
 """Config-5-style stress: K device frames per step (msg_watershed_colorize_batch_dev) with up to
 `inflight` floods in flight; counts steps that raise and frames whose labels differ from the
-first clean step.  usage: python scripts/stress_inflight_dev.py [steps] [K] [inflight] [size]"""
+same frames flooded one at a time (inflight 1); exit 1 if any.  usage: python scripts/stress_inflight_dev.py [steps] [K] [inflight] [size]"""
 import os
 import sys
 
@@ -25,8 +25,11 @@ def main():
     labs = [torch.empty_like(m) for m in mks]
     dsts = [torch.empty((S, S, 3), dtype=torch.uint8, device=dev) for _ in fr]
     seg = msegment.Segmenter(0)
+    seg.set_batch_inflight(1)  # reference labels: one flood at a time on the context itself
+    seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)
+    torch.cuda.synchronize()
+    ref = [x.clone() for x in labs]
     seg.set_batch_inflight(inflight)
-    ref = None
     errs = bad = 0
     for s in range(steps):
         try:
@@ -36,17 +39,15 @@ def main():
             errs += 1
             print("step %d: %s" % (s, e), flush=True)
             continue
-        if ref is None:
-            ref = [x.clone() for x in labs]
-        else:
-            for k in range(K):
-                if not torch.equal(ref[k], labs[k]):
-                    bad += 1
-                    print("step %d frame %d differs" % (s, k), flush=True)
+        for k in range(K):
+            if not torch.equal(ref[k], labs[k]):
+                bad += 1
+                print("step %d frame %d differs" % (s, k), flush=True)
     print("K %d inflight %d size %d: %d error steps, %d bad frames in %d steps" % (K, inflight, S, errs, bad, steps),
           flush=True)
     seg.close()
+    return 1 if errs or bad else 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

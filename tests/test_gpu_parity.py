@@ -286,3 +286,20 @@ def test_picture_service_mirror(seg):
     assert np.array_equal(dst, ws_oracle.colorize(want, d, generate_bgr_palette(d, 99)))
     work = m.copy()
     assert np.array_equal(ps.watershed(img, work, d, False), ws_oracle.colorize(want, d, None))
+
+
+def test_batch_inflight_more_hw_queues():
+    """Regression: with more hardware queues than the default 4, 8 concurrent 4096^2 floods used
+    to time out in k_resolve's cross-rank waits (their grids were not all co-resident); run_batch
+    now splits the co-resident budget between min(inflight, GPU_MAX_HW_QUEUES) floods.  Runs in a
+    child process (the queue count is fixed when HIP initialises); labels must equal the same
+    frames flooded one at a time."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "stress_inflight_dev.py"),
+                        "2", "8", "8", "4096"], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "0 error steps, 0 bad frames" in r.stdout
