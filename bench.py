@@ -212,6 +212,36 @@ def batch_throughput(seg, args, S, seed, sync, steps=5, warmup=2):
                     % (K, seed, seed + K - 1)}
 
 
+def batch_cpu_threads(K):
+    """Threads for the batch CPU baseline: OMP_NUM_THREADS (16 on the GPU boxes), at most 16, at
+    most one per frame."""
+    n = int(os.environ.get("OMP_NUM_THREADS", "8") or 8)
+    return max(1, min(n, 16, K))
+
+
+def cpu_baseline_batch(kind, S, seed, K):
+    """SURVEY 8(d) batch baseline: the same K frames, one frame per thread (the C oracle runs
+    without the GIL inside ctypes), aggregate Mpx/s over one pass of the batch."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from msegment import synth
+    from oracle import ws_oracle
+
+    nt = batch_cpu_threads(K)
+    fr = [synth.frame(kind, S, S, seed + k) for k in range(K)]
+
+    def one(f):
+        ws_oracle.colorize(ws_oracle.watershed(f[0], f[1]), f[2], None)
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(nt) as ex:
+        list(ex.map(one, fr))
+    dt = time.perf_counter() - t0
+    return {"value": round(K * S * S / dt / 1e6, 3), "unit": "Mpx/s", "cores": nt, "kind": "port",
+            "sample": "%d %s %dx%d frames (seeds %d..%d), one frame per thread: oracle/ws_oracle.c "
+                      "watershed + colorize, %.1f s" % (K, kind, S, S, seed, seed + K - 1, dt)}
+
+
 def colour_distance(seg, t_img, img, S, sync, reps=20, check=True):
     """The stand-alone colour-distance stencil (msg_edge_weights_dev) on the bench
     frame: HIP-event-timed launches, 5 algorithmic bytes per pixel (3 in, 2 out); its output is
@@ -391,6 +421,8 @@ def main(argv=None):
     batch = None
     if K == 1 and not NC and not SHAPE and args.batch_frames > 1:
         batch = batch_throughput(seg, args, S, seed, sync)
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            batch["cpu_baseline"] = cpu_baseline_batch(args.kind, S, seed, args.batch_frames)
 
     pcie = None
     if rank == 0 and world == 1 and not NC and not SHAPE:
