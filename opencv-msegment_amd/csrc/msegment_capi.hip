@@ -735,9 +735,15 @@ int msg_edge_weights_dev(msg_ctx* c, const void* d_bgr, void* d_wright, void* d_
   hipStream_t st = stream ? (hipStream_t)stream : c->own;
   const bool vec = cols % 16 == 0 && (((uintptr_t)d_bgr | (uintptr_t)d_wright | (uintptr_t)d_wdown) & 15) == 0;
   if (vec) {
-    const long long th = (long long)((rows + EW_ROWS - 1) / EW_ROWS) * (cols / 16);
-    LAUNCH(c, KID_EDGE, st, k_edge_weights16, dim3((unsigned)((th + 255) / 256)), dim3(256), 0,
-           (const uint8_t*)d_bgr, (uint8_t*)d_wright, (uint8_t*)d_wdown, rows, cols);
+    if (N <= (8ll << 20) * 4) {  // up to 2 x 4096^2 pixels: 2 rows per thread (ws_kernels.hip)
+      const long long th = (long long)((rows + 1) / 2) * (cols / 16);
+      LAUNCH(c, KID_EDGE, st, k_edge_weights16<2>, dim3((unsigned)((th + 255) / 256)), dim3(256), 0,
+             (const uint8_t*)d_bgr, (uint8_t*)d_wright, (uint8_t*)d_wdown, rows, cols);
+    } else {
+      const long long th = (long long)((rows + 3) / 4) * (cols / 16);
+      LAUNCH(c, KID_EDGE, st, k_edge_weights16<4>, dim3((unsigned)((th + 255) / 256)), dim3(256), 0,
+             (const uint8_t*)d_bgr, (uint8_t*)d_wright, (uint8_t*)d_wdown, rows, cols);
+    }
   } else {
     const long long th = (N + 3) / 4;
     LAUNCH(c, KID_EDGE, st, k_edge_weights, dim3((unsigned)((th + 255) / 256)), dim3(256), 0,

@@ -60,10 +60,15 @@ __device__ __forceinline__ void st_granule(unsigned long long* p, unsigned long 
 // fused into k_prep): wr[p] = L-inf BGR distance to the right neighbour, wd[p] to the one below,
 // 0 past the edge.  5 algorithmic bytes per pixel (3 in, 2 out).
 //
-// k_edge_weights16: rows whose width is a multiple of 16 (and 16-B aligned buffers): one thread =
-// a 16-pixel column segment of EW_ROWS rows: EW_ROWS + 1 rows of three 16-B loads (the extra row
-// is the next strip's first: 1.25x reads), one dword per row for the right neighbour of pixel
-// 15, one 16-B store per output row.  k_edge_weights: any shape, 4 pixels per thread.
+// k_edge_weights16<R>: rows whose width is a multiple of 16 (and 16-B aligned buffers): one
+// thread = a 16-pixel column segment of R rows: R + 1 rows of three 16-B loads (the extra row is
+// the next strip's first), one dword per row for the right neighbour of pixel 15, one 16-B store
+// per output row.  Blocks are renumbered XCD-aware (blocks b, b + 8, ... run on one XCD under
+// round-robin placement and get consecutive strips), so the extra row is mostly the one that
+// XCD's L2 just fetched for its neighbour strip: R = 2 is fastest at 4096^2 (20.6 vs 22.6 us for
+// R = 4 without the renumbering), R = 4 at 8192^2 and above (scripts/exp/stencil_variants.hip;
+// staging the rows through LDS for fully contiguous wave loads measured 10-20% slower).
+// k_edge_weights: any shape, 4 pixels per thread.
 __device__ __forceinline__ uint32_t byte_of(const uint32_t* w, int i) { return (w[i >> 2] >> (8 * (i & 3))) & 255u; }
 __device__ __forceinline__ uint32_t linf3(const uint32_t* wa, int ia, const uint32_t* wb, int ib) {
   uint32_t m = 0;
@@ -75,7 +80,6 @@ __device__ __forceinline__ uint32_t linf3(const uint32_t* wa, int ia, const uint
   return m;
 }
 
-constexpr int EW_ROWS = 4;  // rows per thread of k_edge_weights16: 5 row loads for 4 output rows
 
 __device__ __forceinline__ void ld48(const uint8_t* p, uint32_t* w) {
   const uint4* a = reinterpret_cast<const uint4*>(p);
@@ -85,11 +89,15 @@ __device__ __forceinline__ void ld48(const uint8_t* p, uint32_t* w) {
   w[8] = x2.x; w[9] = x2.y; w[10] = x2.z; w[11] = x2.w;
 }
 
+template <int EW_ROWS>
 __global__ __launch_bounds__(256) void k_edge_weights16(const uint8_t* __restrict__ img,
                                                         uint8_t* __restrict__ wr,
                                                         uint8_t* __restrict__ wd, int H, int W) {
   const int segs = W >> 4;
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned b = blockIdx.x;
+  const unsigned per_xcd = gridDim.x / 8;
+  if (b < per_xcd * 8) b = (b % 8) * per_xcd + b / 8;  // a bijection on the first 8*per_xcd blocks
+  const long long t = (long long)b * blockDim.x + threadIdx.x;
   const int strips = (H + EW_ROWS - 1) / EW_ROWS;
   if (t >= (long long)strips * segs) return;
   const int st = (int)(t / segs), sx = (int)(t - (long long)st * segs);

@@ -6,6 +6,7 @@ move a known 8 B per pixel).  Other read widths (random 4-8 B gathers) are uncal
 
   python scripts/pmc_summary.py <dir with pmc_FETCH_SIZE/ and pmc_WRITE_SIZE/> <out.json> [note]
 """
+import re
 import collections
 import csv
 import glob
@@ -21,7 +22,7 @@ def load(path, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            k = r["Kernel_Name"].split("(")[0].replace("msg::", "")
+            k = re.sub(r"<[^>]*>$", "", r["Kernel_Name"].split("(")[0].split()[-1].replace("msg::", ""))
             tot[k] += float(r["Counter_Value"])
             n[k] += 1
     return {k: (tot[k], n[k]) for k in tot}

@@ -1,5 +1,6 @@
 """Per-kernel averages of the counters collected by scripts/pmc_occupancy.sh.
 usage: python scripts/pmc_table.py gpurun_out/<tag> [out.json]"""
+import re
 import collections
 import csv
 import glob
@@ -14,7 +15,7 @@ def main():
     disp = collections.defaultdict(lambda: collections.defaultdict(set))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].replace("msg::", "")
+            k = re.sub(r"<[^>]*>$", "", r["Kernel_Name"].split("(")[0].split()[-1].replace("msg::", ""))
             c = r["Counter_Name"]
             tot[k][c] += float(r["Counter_Value"])
             disp[k][c].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
 """Per-iteration kernel durations of the last flood in a rocprofv3 kernel-trace CSV."""
+import re
 import csv
 import sys
 
@@ -10,7 +11,7 @@ seg = rows[idx[-1]:]
 t0 = int(seg[0]["Start_Timestamp"])
 its, cur, pre = [], None, {}
 for r in seg:
-    k = r["Kernel_Name"].split("(")[0].replace("msg::", "")
+    k = re.sub(r"<[^>]*>$", "", r["Kernel_Name"].split("(")[0].split()[-1].replace("msg::", ""))
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     if k == "k_resolve":
         cur = {"start": int(r["Start_Timestamp"])}

@@ -253,9 +253,10 @@ def test_device_api_torch(seg):
     assert np.array_equal(t_gray.cpu().numpy(), ws_oracle.bgr2gray(col))
 
 
-@pytest.mark.parametrize("shape", [(123, 77), (64, 256), (17, 16), (1, 32), (33, 48), (2, 15)])
+@pytest.mark.parametrize("shape", [(123, 77), (64, 256), (17, 16), (1, 32), (33, 48), (2, 15), (4101, 8192)])
 def test_edge_weights_dev(seg, shape):
-    """Both stencil kernels: width % 16 == 0 takes the 16-pixel vector path."""
+    """Both stencil kernels: width % 16 == 0 takes the 16-pixel vector path (2 rows per thread up to
+    2 x 4096^2 pixels, 4 above: the 4101 x 8192 case, with a ragged last strip)."""
     import torch
 
     H, W = shape
