@@ -183,7 +183,9 @@ def cpu_baseline_shape(img, budget_s=12.0, max_reps=10, rows=512):
 
 def batch_throughput(seg, args, S, seed, sync, steps=5, warmup=2):
     """BASELINE config 5 on this GPU: --batch-frames frames of the same workload per call, up to
-    --inflight floods in flight (msg_watershed_colorize_batch_dev); whole-batch Mpx/s."""
+    --inflight floods in flight (msg_watershed_colorize_batch_dev); whole-batch Mpx/s.  `seed` is
+    the first frame's seed: SURVEY 8(d) numbers config 5's 64 frames 100+k, k = 0..63, so rank r
+    of 8 takes frames 100 + 8r .. 100 + 8r + 7."""
     import torch
 
     from msegment import synth
@@ -420,9 +422,10 @@ def main(argv=None):
 
     batch = None
     if K == 1 and not NC and not SHAPE and args.batch_frames > 1:
-        batch = batch_throughput(seg, args, S, seed, sync)
+        bseed = 100 + rank * args.batch_frames
+        batch = batch_throughput(seg, args, S, bseed, sync)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            batch["cpu_baseline"] = cpu_baseline_batch(args.kind, S, seed, args.batch_frames)
+            batch["cpu_baseline"] = cpu_baseline_batch(args.kind, S, bseed, args.batch_frames)
 
     pcie = None
     if rank == 0 and world == 1 and not NC and not SHAPE:

@@ -82,11 +82,12 @@ def test_no_contours_returns_quietly(tmp_path):
 
 @pytest.mark.gpu
 def test_cli_shape_pipeline_matches_service(tmp_path):
+    """BASELINE config 1: a 256x256 PNG of the mosaic (seed 0) through the CLI."""
     from msegment.picture_service import PictureService
 
     from msegment import synth
 
-    img, _, _ = synth.frame("mosaic", 192, 160, 11)
+    img, _, _ = synth.frame("mosaic", 256, 256, 0)
     cli.write_png(os.path.join(str(tmp_path), "m.png"), img)
     out = io.StringIO()
     rc = cli.run([str(tmp_path), str(tmp_path), "m.png", "--save", "--seed", "4"], out=out)
