@@ -44,7 +44,7 @@ METRIC_SHAPE = "Mpixels/sec segmented by shapeAutoMarkerWatershed (marker stage 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
 # Algorithmic bytes (DESIGN.md "Kernels"): what each kernel must move at minimum per unit.
-BYTES_PER_PIXEL = {"k_prep": 15.0, "k_untile": 15.0, "k_colorize": 7.0, "k_edge_weights": 5.0,
+BYTES_PER_PIXEL = {"k_prep": 15.0, "k_untile": 11.0, "k_colorize": 7.0, "k_edge_weights": 5.0,
                    "k_gray_hist": 4.0, "k_nc_markers": 5.0,
                    # shape marker stage: 1 B in + 1 B out per pixel for the 8-bit stencils
                    "k_gray": 4.0, "k_median": 2.0, "k_canny_nms": 2.0, "k_ring_median3": 2.0}

@@ -35,8 +35,10 @@ struct msg_ctx {
   Ctl* d_ctl = nullptr;
   // flood workspace (sized for cap_n pixels, cap_np tiled pixel words, cap_rc raster chunks)
   long long cap_n = 0, cap_np = 0, cap_rc = 0;
-  int32_t* d_px_base = nullptr;  // tiled {state, w4} words, with a one-tile-row margin each side
-  int32_t* d_px = nullptr;       // = d_px_base + margin
+  // tiled states [0, cap_np) then tiled weights [cap_np, 2 cap_np), each with a one-tile-row
+  // margin either side of the frame's tiles
+  int32_t* d_px_base = nullptr;
+  int32_t* d_px = nullptr;       // states of the frame's tiles = d_px_base + margin
   int32_t *d_qbuf = nullptr, *d_ilist = nullptr;
   int32_t *d_cnt = nullptr, *d_coff = nullptr, *d_tot = nullptr, *d_choff = nullptr;
   unsigned* d_capp = nullptr;  // CAP_SLOTS x NQ
@@ -177,7 +179,7 @@ void free_stage(msg_ctx* c) {
   c->stage_n = 0;
 }
 
-long long tile_margin(int W) { return 16ll * ((W + 3) / 4 + 1); }  // tiled words
+long long tile_margin(int W) { return 16ll * ((W + 3) / 4 + 1); }  // tiled entries
 
 int ensure_flood(msg_ctx* c, int H, int W, hipStream_t st) {
   const long long N = (long long)H * W;
@@ -190,7 +192,7 @@ int ensure_flood(msg_ctx* c, int H, int W, hipStream_t st) {
   free_flood(c);
   const long long nch = (n + CH - 1) / CH;
   const long long qcap = 4 * n + 16;
-  HIPCHK(c, hipMalloc((void**)&c->d_px_base, np * 8));
+  HIPCHK(c, hipMalloc((void**)&c->d_px_base, np * 8));  // np states + np weights
   // stream-ordered: a null-stream hipMemset does not order with the non-blocking flood stream
   // and could land after k_prep's first writes (seen as an all-zero label map / ERR_STATE on
   // the first flood of a fresh batch sub-context)
@@ -266,8 +268,9 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   }
   Ws ws;
   ws.img = d_img;
-  c->d_px = c->d_px_base + 2 * tile_margin(W);  // margin in words of 8 B = 2 ints
+  c->d_px = c->d_px_base + tile_margin(W);
   ws.mk = c->d_px;
+  ws.w4 = c->d_px_base + c->cap_np + tile_margin(W);
   ws.marg = (int)tile_margin(W);
   ws.qbuf = c->d_qbuf;
   ws.ilist = c->d_ilist;

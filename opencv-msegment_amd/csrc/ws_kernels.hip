@@ -17,9 +17,12 @@
 //     scatter), so every bucket stays in exact serial FIFO order.
 //
 // Data in HBM (N = rows*cols pixels; details in DESIGN.md section 4):
-//   mk   u64[tiles*16] TILED flood words {state, w4}: 4x4-pixel tiles (one 128-B line each),
-//                  state >0 label, 0 unknown, -1 WSHED/frame, phase-1 marker, <= -3 queued at
-//                  slot -3-s; w4 = the four L-inf BGR distances to the L,R,T,B neighbours
+//   mk   i32[tiles*16] TILED pixel states, 4x4-pixel tiles in tile-row-major order, so one
+//                  128-B line holds two horizontally adjacent tiles (8x4 pixels): state >0
+//                  label, 0 unknown, -1 WSHED/frame, phase-1 marker, <= -3 queued at slot -3-s
+//   w4   u32[tiles*16] the same tiling: the four L-inf BGR distances to the L,R,T,B neighbours
+//                  (read only for a batch item itself, so the radius-2 state reads of
+//                  k_resolve touch 32-pixel lines)
 //   qbuf int32[..] 256 bucket FIFOs of tiled pixel indices, bucket L = qbuf[qbase[L] + head[L]
 //                  .. qbase[L] + tail[L]), sized exactly by a per-level histogram of each
 //                  pixel's distinct interior edge weights
@@ -152,7 +155,7 @@ __global__ __launch_bounds__(256) void k_edge_weights(const uint8_t* __restrict_
 // ---------------------------------------------------------------------------------------------
 // Phase 0 + phase 1 of cv::watershed (border, sanitise, initial queue levels) fused with the
 // colour-distance stencil and the bucket-capacity histogram.  One thread = one 4x4 tile (its
-// 128-B line of {state, w4} words written with 16-B stores), one block = a 4-row x RSEG-column
+// states and weights written with 16-B stores into mk and w4), one block = a 4-row x RSEG-column
 // strip, i.e. 4 raster chunks, whose phase-1 counts feed the raster-order compaction.
 __device__ __forceinline__ uint32_t ld_bgr(const uint8_t* img, int r, int c, int H, int W) {
   if (r < 0 || r >= H || c < 0 || c >= W) return 0;
@@ -307,9 +310,9 @@ __global__ __launch_bounds__(RSEG) void k_prep(Ws ws, const int32_t* __restrict_
       sv[rx] = state;
       wv4[rx] = w4;
     }
-    int4* out = reinterpret_cast<int4*>(ws.mk + ((((tr * Wt + tc) << 4) + 4 * ry) << 1));
-    out[0] = make_int4(sv[0], (int)wv4[0], sv[1], (int)wv4[1]);
-    out[1] = make_int4(sv[2], (int)wv4[2], sv[3], (int)wv4[3]);
+    const long long to = ((long long)(tr * Wt + tc) << 4) + 4 * ry;
+    *reinterpret_cast<int4*>(ws.mk + to) = make_int4(sv[0], sv[1], sv[2], sv[3]);
+    *reinterpret_cast<int4*>(ws.w4 + to) = make_int4((int)wv4[0], (int)wv4[1], (int)wv4[2], (int)wv4[3]);
   }
   if (run_n) atomicAdd(&caph[run_w], run_n);
   // ---- phase-1 pixels of each of the 4 raster chunks (rows), in raster order, into scratch at
@@ -671,7 +674,7 @@ __global__ __launch_bounds__(256) void k_compact(Ws ws, int nrc) {
   }
 }
 
-__device__ __forceinline__ int ld_state(const Ws& ws, long long t) { return ws.mk[t << 1]; }
+__device__ __forceinline__ int ld_state(const Ws& ws, long long t) { return ws.mk[t]; }
 // 32-bit form of nb_of for indices taken from the margin start (a multiple of 16: tile-aligned)
 __device__ __forceinline__ int nbi(int t, int d, int Wt) {
   const int row = Wt << 4;
@@ -682,9 +685,9 @@ __device__ __forceinline__ int nbi(int t, int d, int Wt) {
     default: return ((t & 12) != 12) ? t + 4 : t + row - 12;
   }
 }
-__device__ __forceinline__ void st_state(const Ws& ws, long long t, int v) { ws.mk[t << 1] = v; }
+__device__ __forceinline__ void st_state(const Ws& ws, long long t, int v) { ws.mk[t] = v; }
 __device__ __forceinline__ unsigned ld_w4(const Ws& ws, long long t) {
-  return (unsigned)ws.mk[(t << 1) | 1];
+  return (unsigned)ws.w4[t];
 }
 
 __device__ __forceinline__ int fold_lab(int lab, int v) {
@@ -714,19 +717,19 @@ __device__ __forceinline__ void gather_item(const Ws& ws, const Seg* segs, int n
   // other neighbours (push competitors), needed only when the neighbour is a 0-pixel, i.e.
   // interior; otherwise the value is discarded (the buffer has a one-tile-row margin either side).
   // Offsets are taken from the margin's start, so they are non-negative and fit 32 bits.
-  const int32_t* const mkb = ws.mk - 2 * (long long)ws.marg;
+  const int32_t* const mkb = ws.mk - ws.marg;
   const int pb = p + ws.marg;  // tiled index relative to the margin start
   int v[4], vo[4][3];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     const int n = nbi(pb, d, Wt);
-    v[d] = mkb[(unsigned)n << 1];
+    v[d] = mkb[(unsigned)n];
     const int e0 = (d == 1) ? 1 : 0;  // directions ascending, skipping the way back to p
     const int e1 = (d <= 1) ? 2 : 1;
     const int e2 = (d == 2) ? 2 : 3;
-    vo[d][0] = mkb[(unsigned)nbi(n, e0, Wt) << 1];
-    vo[d][1] = mkb[(unsigned)nbi(n, e1, Wt) << 1];
-    vo[d][2] = mkb[(unsigned)nbi(n, e2, Wt) << 1];
+    vo[d][0] = mkb[(unsigned)nbi(n, e0, Wt)];
+    vo[d][1] = mkb[(unsigned)nbi(n, e1, Wt)];
+    vo[d][2] = mkb[(unsigned)nbi(n, e2, Wt)];
   }
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
@@ -1798,8 +1801,8 @@ __global__ __launch_bounds__(256) void k_untile(const int32_t* __restrict__ mk, 
                                                 int32_t* __restrict__ lab, int depth,
                                                 const uint8_t* __restrict__ pal,
                                                 uint8_t* __restrict__ dst, uint8_t* __restrict__ gray) {
-  // lane = one 16-B unit {state, w4, state, w4} = 2 pixels of a tile row: loads are lane-
-  // contiguous, and the 16 lanes of one tile row of 8 consecutive tiles store 128 B of labels
+  // lane = one 8-B unit of two states = 2 pixels of a tile row: loads are lane-contiguous, and
+  // the 16 lanes of one tile row of 8 consecutive tiles store 128 B of labels
   extern __shared__ __attribute__((aligned(16))) uint32_t spal[];
   const bool lds_pal = dst != nullptr && pal != nullptr && depth <= PAL_LDS_MAX;
   if (lds_pal) {
@@ -1818,8 +1821,8 @@ __global__ __launch_bounds__(256) void k_untile(const int32_t* __restrict__ mk, 
     const int k = (int)(u & 7);
     const int r = (int)(tt / Wt) * 4 + (k >> 1), c = (int)(tt % Wt) * 4 + 2 * (k & 1);
     if (r >= H || c >= W) continue;
-    const int4 a = reinterpret_cast<const int4*>(mk)[u];
-    const int l[2] = {a.x, a.z};
+    const int2 a = reinterpret_cast<const int2*>(mk)[u];
+    const int l[2] = {a.x, a.y};
     const long long q = (long long)r * W + c;
     const bool both = c + 1 < W;
     if (both && v2) *reinterpret_cast<int2*>(lab + q) = make_int2(l[0], l[1]);

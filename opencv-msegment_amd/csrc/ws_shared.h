@@ -106,7 +106,8 @@ struct Ctl {
 
 struct Ws {
   const uint8_t* img;
-  int32_t* mk;       // TILED pixel words (see tix): state at mk[2t], 4 packed weights at mk[2t+1]
+  int32_t* mk;       // TILED pixel states (see tix): state of tiled pixel t at mk[t]
+  int32_t* w4;       // the same tiling: 4 packed 8-bit weights (L,R,T,B) of pixel t at w4[t]
   int32_t* qbuf;     // bucket regions of tiled pixel indices
   int32_t* ilist;
   unsigned long long* tl;
@@ -122,7 +123,7 @@ struct Ws {
   int* hmir;         // host-mapped progress mirror {iteration, done, error, remaining} (k_scatter)
   int H, W;
   int Wt;            // tiles per tile row = ceil(W / 4)
-  int marg;          // tiled words of margin before mk (mk - 2*marg is the allocation start)
+  int marg;          // tiled entries of margin before mk / w4 (mk - marg starts the state array)
   int nseg;          // raster chunks per image row = ceil(W / RSEG)
   long long N;
   long long qcap;
