@@ -703,6 +703,10 @@ struct Item {
   int dep[16];       // 0..3 label deps, 4+3d+k push deps (earlier items adjacent to the d-target)
 };
 
+// LEAN (k_resolve): the competitors of 0-neighbours only, in a second round of loads.  Otherwise
+// (the one-workgroup small-batch loops, where each batch is a chain of dependent round trips) the
+// whole radius-2 diamond in one round, the values of non-0 neighbours' competitors discarded.
+template <bool LEAN>
 __device__ __forceinline__ void gather_item(const Ws& ws, const Seg* segs, int nseg, int i, int slot,
                                             Item& it) {
   const int Wt = ws.Wt;
@@ -713,23 +717,26 @@ __device__ __forceinline__ void gather_item(const Ws& ws, const Seg* segs, int n
 #pragma unroll
   for (int k = 0; k < 16; ++k) it.dep[k] = -1;
   it.wts = ld_w4(ws, p);
-  // one round of loads for the whole radius-2 diamond: the 4 neighbours and, for each, its 3
-  // other neighbours (push competitors), needed only when the neighbour is a 0-pixel, i.e.
-  // interior; otherwise the value is discarded (the buffer has a one-tile-row margin either side).
-  // Offsets are taken from the margin's start, so they are non-negative and fit 32 bits.
+  // the 4 neighbours and their 3 other neighbours (push competitors, needed only for a 0-pixel
+  // neighbour: LEAN loads them after the neighbours, for 0-pixels only, since k_resolve is bound
+  // by the new lines it fetches per item -- DESIGN.md section 6).  Offsets are taken from the
+  // margin's start (the buffer has a one-tile-row margin either side), so they are non-negative
+  // and fit 32 bits.
   const int32_t* const mkb = ws.mk - ws.marg;
   const int pb = p + ws.marg;  // tiled index relative to the margin start
-  int v[4], vo[4][3];
+  int v[4], nn[4], vo[4][3];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    const int n = nbi(pb, d, Wt);
-    v[d] = mkb[(unsigned)n];
-    const int e0 = (d == 1) ? 1 : 0;  // directions ascending, skipping the way back to p
-    const int e1 = (d <= 1) ? 2 : 1;
-    const int e2 = (d == 2) ? 2 : 3;
-    vo[d][0] = mkb[(unsigned)nbi(n, e0, Wt)];
-    vo[d][1] = mkb[(unsigned)nbi(n, e1, Wt)];
-    vo[d][2] = mkb[(unsigned)nbi(n, e2, Wt)];
+    nn[d] = nbi(pb, d, Wt);
+    v[d] = mkb[(unsigned)nn[d]];
+    if (!LEAN) {
+      const int e0 = (d == 1) ? 1 : 0;  // directions ascending, skipping the way back to p
+      const int e1 = (d <= 1) ? 2 : 1;
+      const int e2 = (d == 2) ? 2 : 3;
+      vo[d][0] = mkb[(unsigned)nbi(nn[d], e0, Wt)];
+      vo[d][1] = mkb[(unsigned)nbi(nn[d], e1, Wt)];
+      vo[d][2] = mkb[(unsigned)nbi(nn[d], e2, Wt)];
+    }
   }
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
@@ -743,6 +750,18 @@ __device__ __forceinline__ void gather_item(const Ws& ws, const Seg* segs, int n
     }
   }
   if (it.base_lab == WSHED) return;  // WSHED absorbs: no label or push dependency matters
+  if (LEAN) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int e0 = (d == 1) ? 1 : 0;
+      const int e1 = (d <= 1) ? 2 : 1;
+      const int e2 = (d == 2) ? 2 : 3;
+      const bool z = (it.zero_mask >> d) & 1u;
+      vo[d][0] = z ? mkb[(unsigned)nbi(nn[d], e0, Wt)] : 0;
+      vo[d][1] = z ? mkb[(unsigned)nbi(nn[d], e1, Wt)] : 0;
+      vo[d][2] = z ? mkb[(unsigned)nbi(nn[d], e2, Wt)] : 0;
+    }
+  }
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     if (!((it.zero_mask >> d) & 1u)) continue;
@@ -840,7 +859,7 @@ __global__ __launch_bounds__(RBS, 6) void k_resolve(Ws ws) {
     int sg = 0;
     if (valid) {
       sg = (B.nseg == 1) ? 0 : seg_of_rank(segs, B.nseg, i);
-      gather_item(ws, segs, B.nseg, i, segs[sg].bstart + (i - segs[sg].rank), it);
+      gather_item<true>(ws, segs, B.nseg, i, segs[sg].bstart + (i - segs[sg].rank), it);
       ws.ipx[i] = (int32_t)it.p;
     } else {
       it.p = 0;
@@ -1353,7 +1372,7 @@ __device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qba
     int sg = 0;
     if (valid) {
       sg = (B.nseg == 1) ? 0 : seg_of_rank(s_seg, B.nseg, i);
-      gather_item(ws, s_seg, B.nseg, i, s_seg[sg].bstart + (i - s_seg[sg].rank), it);
+      gather_item<false>(ws, s_seg, B.nseg, i, s_seg[sg].bstart + (i - s_seg[sg].rank), it);
     } else {
       it.p = 0;
       it.base_lab = WSHED;
@@ -1545,7 +1564,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
       int sg = 0;
       if (valid) {
         sg = (B.nseg == 1) ? 0 : seg_of_rank(s_seg, B.nseg, i);
-        gather_item(ws, s_seg, B.nseg, i, s_seg[sg].bstart + (i - s_seg[sg].rank), it);
+        gather_item<false>(ws, s_seg, B.nseg, i, s_seg[sg].bstart + (i - s_seg[sg].rank), it);
       }
       bool pending = valid;
       long long t0 = 0;
