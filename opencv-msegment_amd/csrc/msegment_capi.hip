@@ -329,7 +329,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
       // fewer queued items -> fewer batches left: shrink the group so that the iterations
       // enqueued past the end of the flood (no-ops, but each still a launch) stay few
       const int rem = c->h_mir[3];
-      c->group = rem > (1 << 20) ? 8 : rem > (1 << 17) ? 4 : rem > (1 << 14) ? 2 : 1;
+      c->group = rem > (1 << 21) ? 8 : rem > (1 << 19) ? 4 : rem > (1 << 17) ? 2 : 1;
     }
     prev_end = it - 1;
   }
