@@ -17,14 +17,19 @@ run() {
   tail -n 8 "$OUT/$name.log"
   case $rc in 0|1|5) return 0 ;; *) echo "STOP after $name (rc=$rc)"; exit "$rc" ;; esac
 }
-run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-run pytest_gpu 900 python -m pytest tests -m gpu -x -q
-run bench 600 python bench.py "$@"
-[ -n "${EXTRA_BENCH:-}" ] && run bench_extra 600 python bench.py $EXTRA_BENCH
-run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass
+if [ -z "${PROF_ONLY:-}" ]; then
+  run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
+  run pytest_gpu 900 python -m pytest tests -m gpu -x -q
+  run bench 600 python bench.py "$@"
+  [ -n "${EXTRA_BENCH:-}" ] && run bench_extra 600 python bench.py $EXTRA_BENCH
+fi
+# the profiled command is the headline's single-flood path only (--batch-frames 1: no concurrent
+# floods, whose overlapping kernels would inflate the per-launch durations and traffic)
+PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass --batch-frames 1"
+run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py $PROF_ARGS
 find "$OUT/prof" -name '*stats*' -exec cp {} "$OUT/" \; 2>/dev/null
 # HBM traffic: one counter group per rocprofv3 run, kernel trace only (MI355X_MICROARCH.md)
 for ctr in FETCH_SIZE WRITE_SIZE; do
-  run pmc_$ctr 600 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_$ctr" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass
+  run pmc_$ctr 600 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_$ctr" -o run -- python bench.py $PROF_ARGS
 done
 echo "== done"
