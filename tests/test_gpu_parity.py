@@ -304,3 +304,36 @@ def test_batch_inflight_more_hw_queues():
                         "2", "8", "8", "4096"], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "0 error steps, 0 bad frames" in r.stdout
+
+
+def test_c_abi_error_paths(seg):
+    """The C ABI's CV_Assert-like checks (include/msegment.h): each bad call returns MSG_EINVAL
+    with a message and leaves the context usable."""
+    import ctypes
+
+    from msegment import _lib
+
+    L, h = seg._L, seg._h
+    img = np.zeros((8, 8, 3), np.uint8)
+    mk = np.zeros((8, 8), np.int32)
+    mk[4, 4] = 1
+    ip = img.ctypes.data_as(ctypes.c_void_p)
+    mp = mk.ctypes.data_as(ctypes.c_void_p)
+    bad = [
+        lambda: L.msg_watershed(h, ip, 24, mp, 32, -1, 8),          # negative rows
+        lambda: L.msg_watershed(h, ip, 24, mp, 32, 1 << 15, 1 << 14),  # > 2^28 pixels
+        lambda: L.msg_watershed(h, None, 24, mp, 32, 8, 8),         # null image
+        lambda: L.msg_watershed(h, ip, 23, mp, 32, 8, 8),           # bgr stride < 3 cols
+        lambda: L.msg_watershed(h, ip, 24, mp, 30, 8, 8),           # marker stride not 4-aligned
+        lambda: L.msg_watershed_colorize(h, ip, 24, mp, 32, 8, 8, -1, None,
+                                         img.ctypes.data_as(ctypes.c_void_p), 24, None, 0),  # depth < 0
+        lambda: L.msg_set_batch_inflight(h, 0),
+    ]
+    for k, call in enumerate(bad):
+        assert call() == _lib.MSG_EINVAL, k
+        assert L.msg_last_error(h), k
+    out = mk.copy()
+    assert L.msg_watershed(h, ip, 24, out.ctypes.data_as(ctypes.c_void_p), 32, 8, 8) == 0
+    assert np.array_equal(out, ws_oracle.watershed(img, mk))
+    # empty frames are a no-op, not an error
+    assert L.msg_watershed(h, ip, 24, mp, 32, 0, 8) == 0
