@@ -108,9 +108,11 @@ def main():
     print("wrote", len(names), "small cases")
 
 
-# (kind, H, W, seed): SURVEY.md §8d seeds -- cfg2 1024^2 s=1, cfg3 4096^2 s=2, cfg4 16384^2 s=3
+# (kind, H, W, seed): SURVEY.md §8d seeds -- cfg2 1024^2 s=1, cfg3 4096^2 s=2, cfg4 16384^2 s=3,
+# cfg5's first frame 4096^2 s=100; plus a large frame with ragged 4x4 tiles in both directions
 DIGEST_CASES = [("mosaic", 1024, 1024, 1), ("mosaic_noise", 1024, 1024, 1),
-                ("random", 512, 512, 3), ("mosaic", 4096, 4096, 2), ("mosaic", 16384, 16384, 3)]
+                ("random", 512, 512, 3), ("mosaic", 4096, 4096, 2), ("mosaic", 16384, 16384, 3),
+                ("mosaic", 4096, 4096, 100), ("mosaic", 3001, 5003, 7)]
 
 
 def write_digests(only=None):

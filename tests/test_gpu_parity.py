@@ -129,6 +129,39 @@ def test_config4_16384_mosaic_digest_single_gpu(seg):
     assert int((out == -1).sum()) == dg["wshed_pixels"]
 
 
+def test_large_ragged_mosaic_digest(seg):
+    """3001 x 5003: ragged 4x4 tiles in both directions (3001 % 4 == 1, 5003 % 4 == 3) at 15 M
+    pixels, against the oracle's digest, plus the invariants."""
+    dg = json.load(open(os.path.join(GOLD, "digests.json")))["mosaic_3001x5003_s7"]
+    img, m, d = synth.frame("mosaic", 3001, 5003, 7)
+    out = gpu_ws(seg, img, m)
+    assert hashlib.sha256(out.tobytes()).hexdigest() == dg["labels_sha256"]
+    check_properties(m, out)
+
+
+def test_config5_frames_batch_vs_digest(seg):
+    """BASELINE config 5's frames (4096^2, SURVEY.md seeds 100 + k) through the device batch entry
+    point, 4 floods in flight: frame 0 against the oracle's digest, every frame against the same
+    frame flooded alone."""
+    import torch
+
+    dev = torch.device("cuda", seg.device)
+    dg = json.load(open(os.path.join(GOLD, "digests.json")))["mosaic_4096x4096_s100"]
+    fr = [synth.frame("mosaic", 4096, 4096, 100 + k) for k in range(4)]
+    depth = max(f[2] for f in fr)
+    imgs = [torch.from_numpy(f[0]).to(dev) for f in fr]
+    mks = [torch.from_numpy(f[1]).to(dev) for f in fr]
+    labs = [torch.empty_like(x) for x in mks]
+    dsts = [torch.empty((4096, 4096, 3), dtype=torch.uint8, device=dev) for _ in fr]
+    seg.set_batch_inflight(4)
+    seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)
+    torch.cuda.synchronize()
+    got = [x.cpu().numpy() for x in labs]
+    assert hashlib.sha256(got[0].tobytes()).hexdigest() == dg["labels_sha256"]
+    for k in range(1, 4):
+        assert np.array_equal(got[k], gpu_ws(seg, fr[k][0], fr[k][1])), k
+
+
 def check_properties(m, out):
     """Size-independent watershed invariants."""
     H, W = m.shape
