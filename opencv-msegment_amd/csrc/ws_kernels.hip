@@ -1352,6 +1352,8 @@ __device__ __forceinline__ bool attempt_item_slots(const Item& it, const int (&v
 // wave_rank on the queue state the small loop keeps in LDS (in-order LDS within one wave).
 // Returns when the next batch has more than 64 items, the flood is done, or on error.
 constexpr int TINY_MAX = 64;
+constexpr int SERIAL_RUN = 256;    // serial_loop: clean pops after which batches pay again
+constexpr int SERIAL_SWITCH = 16;  // a tiny batch cut before this many items -> serial_loop
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1359,7 +1361,7 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 __device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qbase, int* s_head, int* s_tail,
-                          int* wrow, int* s_wcap, int* s_err, int* s_nseg, int* s_n, long long* cnt) {
+                          int* wrow, int* s_wcap, int* s_err, int* s_nseg, int* s_n, int* s_ser, long long* cnt) {
   const int lane = lane_id();
   const int Wt = ws.Wt;
   for (;;) {
@@ -1498,8 +1500,144 @@ __device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qba
       nb.bstart = (*s_nseg > 0) ? s_seg[0].bstart : 0;
       *s_B = nb;
       if (*s_nseg > 0) cnt[3] += 1;
+      if (cut != NONE && ncommit < SERIAL_SWITCH) *s_ser = 1;  // interrupt-dense: pop serially
     }
+    wave_sync();
+    if (*s_ser) return;
   }
+}
+
+// Serial pops: cv::watershed's own phase-2 loop (pop the oldest item of the lowest non-empty
+// bucket, fold its labelled neighbours, push its unknown ones in L,R,T,B order), run by wave 0 on
+// the engine's own queue and state, for the interrupt-dense regime where batches commit a few
+// items each.  Every lane executes the same scalar program on the same addresses (uniform loads
+// coalesce to one request; vector atomics keep them off the scalar cache, which does not see
+// vector stores); the lanes only share the work of prefetching the next 64 queue slots of the
+// popped bucket.  Entered when a tiny batch commits fewer than SERIAL_SWITCH items before an
+// interrupt (a pop costs ~0.55 us here against ~7 us per tiny batch: scripts/regime_probe.py);
+// returns once a run of SERIAL_RUN pops pushed nothing below the popped level (batches pay again),
+// or when the queue is empty, forming the next batch.
+
+
+__device__ __forceinline__ int ld_state_v(const Ws& ws, int t) {
+  return __hip_atomic_load(ws.mk + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int ld_qbuf_v(const Ws& ws, int slot) {
+  return __hip_atomic_load(ws.qbuf + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// lowest non-empty bucket at or above `from` (NQ if none); wave-uniform
+__device__ __forceinline__ int lowest_bucket(const int* head, const int* tail, int from) {
+  const int lane = lane_id();
+  int lo = NQ;
+#pragma unroll
+  for (int k = 0; k < NQ / 64; ++k) {
+    const int l = lane * (NQ / 64) + k;
+    if (l >= from && tail[l] > head[l]) lo = min(lo, l);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lo = min(lo, __shfl_xor(lo, o));
+  return lo;
+}
+
+__device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qbase, int* s_head, int* s_tail,
+                            int* s_wcap, int* s_err, int* s_nseg, int* s_n, int* s_ser, long long* cnt) {
+  const int lane = lane_id();
+  const int Wt = ws.Wt, marg = ws.marg;
+  const Batch B0 = *s_B;
+  long long pops = 0, pushes = 0;
+  int run = 0;
+  int lo = lowest_bucket(s_head, s_tail, 0);
+  int ring = 0, ring_l = -1, ring_h0 = 0, ring_n = 0;
+  while (lo < NQ) {
+    const int h = s_head[lo], navail = s_tail[lo] - h;
+    if (navail <= 0) {
+      lo = lowest_bucket(s_head, s_tail, lo + 1);
+      continue;
+    }
+    if (run >= SERIAL_RUN) break;
+    if (lo != ring_l || h >= ring_h0 + ring_n) {  // the bucket's next 64 slots, one load per lane
+      wave_sync();
+      ring_l = lo;
+      ring_h0 = h;
+      ring_n = min(navail, 64);
+      ring = (lane < ring_n) ? ld_qbuf_v(ws, s_qbase[lo] + h + lane) : 0;
+    }
+    const int p = __shfl(ring, h - ring_h0);
+    const int pb = p + marg;
+    int nb[4], st[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      nb[d] = nbi(pb, d, Wt) - marg;
+      st[d] = ld_state_v(ws, nb[d]);
+    }
+    const unsigned w4 = (unsigned)ws.w4[p];
+    int lab = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      if (st[d] > 0) lab = fold_lab(lab, st[d]);
+    if (lab == 0) {  // impossible for an exact queue
+      if (lane == 0) *s_err = ERR_STATE;
+      lab = WSHED;
+    }
+    wave_sync();
+    if (lane == 0) {
+      st_state(ws, p, lab);
+      s_head[lo] = h + 1;
+    }
+    ++pops;
+    bool lower = false;
+    int newlo = lo;
+    if (lab != WSHED) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        if (st[d] != 0) continue;
+        const int t = (int)((w4 >> (8 * d)) & 255u);
+        const int dest = s_qbase[t] + s_tail[t];
+        if (dest < 0 || (long long)dest >= ws.qcap) {
+          if (lane == 0) *s_err = ERR_CAPACITY;
+          continue;
+        }
+        if (lane == 0) {
+          ws.qbuf[dest] = nb[d];
+          st_state(ws, nb[d], queued_state(dest));
+          s_tail[t] = s_tail[t] + 1;
+        }
+        wave_sync();
+        ++pushes;
+        if (t < lo) lower = true;
+        newlo = min(newlo, t);
+      }
+    }
+    run = lower ? 0 : run + 1;
+    lo = newlo;
+    if (*s_err) break;
+  }
+  wave_sync();
+  if (lane == 0) {
+    cnt[0] += pops;
+    cnt[1] += pops;
+    cnt[2] += pushes;
+    *s_wcap = 0;  // the next batch: a whole generation (next_wcap shrinks it again on a cut)
+  }
+  wave_sync();
+  form_batch(s_qbase, s_head, s_tail, 0, 0, s_seg, s_nseg, s_n);
+  wave_sync();
+  if (lane == 0) {
+    Batch nb;
+    nb.mode = 0;
+    nb.epoch = B0.epoch + 1;
+    nb.ncommit = 0;
+    nb.nchunk = 0;
+    nb.nseg = *s_nseg;
+    nb.n = (*s_nseg > 0) ? *s_n : 0;
+    nb.L = (*s_nseg > 0) ? s_seg[0].L : -1;
+    nb.bstart = (*s_nseg > 0) ? s_seg[0].bstart : 0;
+    *s_B = nb;
+    *s_ser = 0;
+    cnt[3] += pops;
+  }
+  wave_sync();
 }
 
 __device__ __forceinline__ void small_loop(const Ws& ws) {
@@ -1511,6 +1649,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
   __shared__ int s_wcnt[NW][NQ];
   __shared__ Seg s_seg[NQ];
   __shared__ int s_cut, s_segcut, s_minpush, s_err, s_nseg, s_n, s_wcap;
+  __shared__ int s_ser;  // 1: the interrupt-dense regime, tiny batches popped serially
   __shared__ Batch s_B;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const int Wt = ws.Wt;
@@ -1518,6 +1657,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     s_B = ctl->bat;
     s_err = ctl->error;
     s_wcap = ctl->wcap;
+    s_ser = 0;
   }
   if (tid < NQ) {
     s_qbase[tid] = ctl->qbase[tid];
@@ -1537,7 +1677,10 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     if (B.n <= TINY_MAX) {  // runs of tiny batches: wave 0 alone, the other waves wait here
       if (wv == 0) {
         long long c4[4] = {0, 0, 0, 0};
-        tiny_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, s_wcnt[0], &s_wcap, &s_err, &s_nseg, &s_n, c4);
+        if (s_ser)
+          serial_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, c4);
+        else
+          tiny_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, s_wcnt[0], &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, c4);
         if (tid == 0) {
           nb_pops += c4[0];
           nb_items += c4[1];
