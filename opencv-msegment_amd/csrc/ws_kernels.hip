@@ -1511,9 +1511,10 @@ __device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qba
 // bucket, fold its labelled neighbours, push its unknown ones in L,R,T,B order), run by wave 0 on
 // the engine's own queue and state, for the interrupt-dense regime where batches commit a few
 // items each.  Every lane executes the same scalar program on the same addresses (uniform loads
-// coalesce to one request; vector atomics keep them off the scalar cache, which does not see
-// vector stores); the lanes only share the work of prefetching the next 64 queue slots of the
-// popped bucket.  Entered when a tiny batch commits fewer than SERIAL_SWITCH items before an
+// and stores coalesce to one request each; vector atomics keep the loads off the scalar cache,
+// which does not see vector stores), so every lane's loads follow its own stores and no wait or
+// barrier is needed between pops; the lanes only share the work of prefetching the next 64 queue
+// slots of the popped bucket.  Entered when a tiny batch commits fewer than SERIAL_SWITCH items before an
 // interrupt (a pop costs ~0.55 us here against ~7 us per tiny batch: scripts/regime_probe.py);
 // returns once a run of SERIAL_RUN pops pushed nothing below the popped level (batches pay again),
 // or when the queue is empty, forming the next batch.
@@ -1557,7 +1558,6 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
     }
     if (run >= SERIAL_RUN) break;
     if (lo != ring_l || h >= ring_h0 + ring_n) {  // the bucket's next 64 slots, one load per lane
-      wave_sync();
       ring_l = lo;
       ring_h0 = h;
       ring_n = min(navail, 64);
@@ -1577,14 +1577,13 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
     for (int d = 0; d < 4; ++d)
       if (st[d] > 0) lab = fold_lab(lab, st[d]);
     if (lab == 0) {  // impossible for an exact queue
-      if (lane == 0) *s_err = ERR_STATE;
+      *s_err = ERR_STATE;
       lab = WSHED;
     }
-    wave_sync();
-    if (lane == 0) {
-      st_state(ws, p, lab);
-      s_head[lo] = h + 1;
-    }
+    // every lane stores the same value to the same address (one request): a later load by the
+    // wave includes the lane's own earlier store, so no wait is needed for the next pop to see it
+    st_state(ws, p, lab);
+    s_head[lo] = h + 1;
     ++pops;
     bool lower = false;
     int newlo = lo;
@@ -1595,15 +1594,12 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
         const int t = (int)((w4 >> (8 * d)) & 255u);
         const int dest = s_qbase[t] + s_tail[t];
         if (dest < 0 || (long long)dest >= ws.qcap) {
-          if (lane == 0) *s_err = ERR_CAPACITY;
+          *s_err = ERR_CAPACITY;
           continue;
         }
-        if (lane == 0) {
-          ws.qbuf[dest] = nb[d];
-          st_state(ws, nb[d], queued_state(dest));
-          s_tail[t] = s_tail[t] + 1;
-        }
-        wave_sync();
+        ws.qbuf[dest] = nb[d];
+        st_state(ws, nb[d], queued_state(dest));
+        s_tail[t] = s_tail[t] + 1;
         ++pushes;
         if (t < lo) lower = true;
         newlo = min(newlo, t);
