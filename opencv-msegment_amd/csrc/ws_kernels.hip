@@ -1352,8 +1352,14 @@ __device__ __forceinline__ bool attempt_item_slots(const Item& it, const int (&v
 // wave_rank on the queue state the small loop keeps in LDS (in-order LDS within one wave).
 // Returns when the next batch has more than 64 items, the flood is done, or on error.
 constexpr int TINY_MAX = 64;
-constexpr int SERIAL_RUN = 256;    // serial_loop: clean pops after which batches pay again
-constexpr int SERIAL_SWITCH = 16;  // a tiny batch cut before this many items -> serial_loop
+#ifndef MSEG_SERIAL_RUN
+#define MSEG_SERIAL_RUN 4096
+#endif
+#ifndef MSEG_SERIAL_SWITCH
+#define MSEG_SERIAL_SWITCH 16
+#endif
+constexpr int SERIAL_RUN = MSEG_SERIAL_RUN;    // serial_loop: clean pops after which batches pay again
+constexpr int SERIAL_SWITCH = MSEG_SERIAL_SWITCH;  // a tiny batch cut before this many items -> serial_loop
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
