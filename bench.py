@@ -38,7 +38,7 @@ os.environ["GPU_MAX_HW_QUEUES"] = str(max(_hwq, 8))
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "opencv-msegment_amd"))
 
-METRIC = "Mpixels/sec segmented at 4096x4096 RGB; achieved HBM GB/s vs peak"
+METRIC = "Mpixels/sec segmented at {S}x{S} RGB; achieved HBM GB/s vs peak"  # BASELINE.json at S = 4096
 METRIC_NC = "Mpixels/sec segmented by notConnectedMarkers (marker stage + watershed + colorByIndexes)"
 METRIC_SHAPE = "Mpixels/sec segmented by shapeAutoMarkerWatershed (marker stage + watershed + colorByIndexes)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
@@ -58,6 +58,22 @@ E2E_BYTES_PER_PIXEL = 14.0                  # 3 B BGR + 4 B markers in, 4 B labe
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def spawn_ranks(n, argv):
+    """`--gpus N` without a launcher: start N rank processes through torch.distributed.run (one
+    per GPU, rendezvous on 127.0.0.1) as children of this process, before anything here touches
+    the GPU, and return their exit code.  The ranks see WORLD_SIZE and do not spawn again."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
 
 
 def dist_env():
@@ -244,7 +260,63 @@ def cpu_baseline_batch(kind, S, seed, K):
                       "watershed + colorize, %.1f s" % (K, kind, S, S, seed, seed + K - 1, dt)}
 
 
-def colour_distance(seg, t_img, img, S, sync, reps=20, check=True):
+def stress_line(seg, S, sync, dev, steps, cpu=True, kind="mosaic_noise", seed=2):
+    """BASELINE config 3's stress variant beside the headline: mosaic+noise SxS seed 2 (the
+    interrupt-dense regime: per-channel noise makes pushes below the popped level every few pops),
+    the same device-resident step, its parity against the committed oracle digest, and the C
+    oracle timed on the same frame (1 thread)."""
+    import numpy as np
+    import torch
+
+    from msegment import synth
+
+    img, m, depth = synth.frame(kind, S, S, seed)
+    t_img = torch.from_numpy(img).to(dev)
+    t_m = torch.from_numpy(m).to(dev)
+    t_lab = torch.empty_like(t_m)
+    t_dst = torch.empty((S, S, 3), dtype=torch.uint8, device=dev)
+    seg.watershed_colorize_dev(t_img, t_m, t_lab, depth, None, t_dst)
+    sync()
+    st = seg.stats()
+    dkey = "%s_%dx%d_s%d" % (kind, S, S, seed)
+    dgs = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
+    lab = t_lab.cpu().numpy()
+    parity = None
+    if dkey in dgs:
+        parity = ("bit-exact vs oracle digest " if hashlib.sha256(lab.tobytes()).hexdigest()
+                  == dgs[dkey]["labels_sha256"] else "MISMATCH vs oracle digest ") + dkey
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        seg.watershed_colorize_dev(t_img, t_m, t_lab, depth, None, t_dst)
+    sync()
+    dt = time.perf_counter() - t0
+    out = {"workload": "%s %dx%d seed %d, watershed + colorByIndexes(colored=false), device-resident "
+                       "(BASELINE config 3 stress variant)" % (kind, S, S, seed),
+           "value": round(S * S * steps / dt / 1e6, 3), "unit": "Mpx/s", "steps": steps,
+           "ms_per_step": round(1000.0 * dt / steps, 3), "parity": parity,
+           "flood": {"batches": st["batches"], "pops": st["pops"], "items": st["items"]}}
+    if cpu:
+        c, cl = cpu_baseline(img, m, depth, budget_s=8.0, max_reps=5)
+        out["cpu_baseline"] = c
+        if parity is None:
+            out["parity"] = "bit-exact vs oracle" if np.array_equal(cl, lab) else "MISMATCH vs oracle"
+    del t_img, t_m, t_lab, t_dst
+    return out
+
+
+def pmc_traffic(kernel, cfg):
+    """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/pmc_latest.json,
+    scripts/pmc_summary.py), only when they were collected on this same workload `cfg`."""
+    if not os.path.exists(PMC_SUMMARY):
+        return None, None
+    pm = json.load(open(PMC_SUMMARY))
+    kk = pm.get("kernels", {}).get(kernel)
+    if not kk or pm.get("config") != cfg:
+        return None, None
+    return round(kk["hbm_bytes_per_launch"]), "profiles/pmc_latest.json (%s; %s)" % (pm.get("correction"), pm.get("note", ""))
+
+
+def colour_distance(seg, t_img, img, S, sync, pmc_cfg, reps=20, check=True):
     """The stand-alone colour-distance stencil (msg_edge_weights_dev) on the bench
     frame: HIP-event-timed launches, 5 algorithmic bytes per pixel (3 in, 2 out); its output is
     checked against numpy on the same frame."""
@@ -275,20 +347,43 @@ def colour_distance(seg, t_img, img, S, sync, reps=20, check=True):
         return None
     avg_us = 1000.0 * total_ms / launches
     gbs = BYTES_PER_PIXEL["k_edge_weights"] * S * S / (avg_us * 1e-6) / 1e9
-    traffic = None
-    if os.path.exists(PMC_SUMMARY):
-        kk = json.load(open(PMC_SUMMARY)).get("kernels", {}).get("k_edge_weights16")
-        if kk:
-            traffic = round(kk["hbm_bytes_per_launch"])
+    traffic, _ = pmc_traffic("k_edge_weights16", pmc_cfg)
     return {"bound": "hbm", "kernel": "k_edge_weights16", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5), "avg_launch_us": round(avg_us, 3),
             "alg_bytes_per_launch": BYTES_PER_PIXEL["k_edge_weights"] * S * S, "traffic": traffic,
             "launches": launches, "parity": None if ok is None else ("bit-exact vs numpy" if ok else "MISMATCH")}
 
 
+def harness_test(args, rank, world):
+    """Test-only (tests/test_dist.py, CPU): the launch / barrier / max-over-ranks / JSON path of
+    this file over gloo with a 5 ms sleep as the step.  Measures nothing about the GPU path and
+    says so in its line; never selected unless MSEG_BENCH_HARNESS_TEST is set."""
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    barrier = (lambda: dist.barrier()) if world > 1 else (lambda: None)
+    for _ in range(args.warmup):
+        time.sleep(0.005)
+    dt = timed_steps(lambda: time.sleep(0.005), args.steps, barrier, lambda: None)
+    dt_max = reduce_max(dt)
+    if rank == 0:
+        print(json.dumps({"metric": "bench.py harness test (no GPU)", "value": round(world * args.steps / dt_max, 3),
+                          "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(1000.0 * dt_max / args.steps, 4), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": None,
+                          "data": "harness test: each rank's step is a 5 ms sleep",
+                          "config": {"workload": "harness test", "parallelism": "replicas%d" % world}}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without a launcher N > 1 spawns them (torch.distributed.run)")
     ap.add_argument("--steps", type=int, default=None, help="default 10 (nc: 2)")
     ap.add_argument("--warmup", type=int, default=None, help="default 3 (nc: 1)")
     ap.add_argument("--size", type=int, default=4096)
@@ -306,6 +401,8 @@ def main(argv=None):
                          "shape: shapeAutoMarkerWatershed's (median, Canny, rings, components)")
     ap.add_argument("--nc-depth", type=int, default=4, help="user depth of the nc pipeline")
     ap.add_argument("--nc-options", default="GISTO_DIAP", help="comma list: GISTO_DIAP,MULTI_OTSU")
+    ap.add_argument("--stress-steps", type=int, default=2,
+                    help="steps of the config-3 stress line (mosaic+noise at --size); 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile-pass", action="store_true")
     args = ap.parse_args(argv)
@@ -315,7 +412,13 @@ def main(argv=None):
     if args.warmup is None:
         args.warmup = 1 if args.pipeline == "nc" else 3
 
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(spawn_ranks(args.gpus, sys.argv[1:] if argv is None else argv))
     rank, world, local = dist_env()
+    if args.gpus is not None and world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%d ranks" % (args.gpus, world))
+    if os.environ.get("MSEG_BENCH_HARNESS_TEST"):
+        return harness_test(args, rank, world)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -333,6 +436,8 @@ def main(argv=None):
 
     S = args.size
     seed = args.seed if args.seed is not None else (2 if world == 1 else 100 + rank)
+    # the workload the PMC passes must have been collected on for their traffic to be quoted
+    pmc_cfg = {"pipeline": args.pipeline, "kind": args.kind, "size": S, "seed": seed, "frames": max(1, args.frames)}
     t0 = time.perf_counter()
     img, m, depth = synth.frame(args.kind, S, S, seed)
     log("[rank %d] generated %s %dx%d seed %d in %.1fs" % (rank, args.kind, S, S, seed, time.perf_counter() - t0))
@@ -418,7 +523,7 @@ def main(argv=None):
 
     stencil = None
     if not NC and not SHAPE and K == 1:
-        stencil = colour_distance(seg, t_img, img, S, sync, check=(rank == 0))
+        stencil = colour_distance(seg, t_img, img, S, sync, pmc_cfg, check=(rank == 0))
 
     batch = None
     if K == 1 and not NC and not SHAPE and args.batch_frames > 1:
@@ -426,6 +531,10 @@ def main(argv=None):
         batch = batch_throughput(seg, args, S, bseed, sync)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             batch["cpu_baseline"] = cpu_baseline_batch(args.kind, S, bseed, args.batch_frames)
+
+    stress = None
+    if rank == 0 and world == 1 and K == 1 and not NC and not SHAPE and args.kind == "mosaic" and args.stress_steps > 0:
+        stress = stress_line(seg, S, sync, dev, args.stress_steps, cpu=not args.no_cpu_baseline)
 
     pcie = None
     if rank == 0 and world == 1 and not NC and not SHAPE:
@@ -457,13 +566,7 @@ def main(argv=None):
         roof = None
         if kern:
             top = kern[0]
-            traffic, tsrc = None, None
-            if os.path.exists(PMC_SUMMARY):  # HBM bytes per launch from the committed PMC passes
-                pm = json.load(open(PMC_SUMMARY))
-                kk = pm.get("kernels", {}).get(top["kernel"])
-                if kk:
-                    traffic = round(kk["hbm_bytes_per_launch"])
-                    tsrc = "profiles/pmc_latest.json (%s; %s)" % (pm.get("correction"), pm.get("note", ""))
+            traffic, tsrc = pmc_traffic(top["kernel"], pmc_cfg)
             roof = {"bound": "hbm", "kernel": top["kernel"], "achieved": top["achieved_gbs"],
                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(top["achieved_gbs"] / HBM_PEAK_GBS, 5) if top["achieved_gbs"] else None,
@@ -471,7 +574,7 @@ def main(argv=None):
                     "alg_bytes_per_launch": top["alg_bytes_per_launch"], "avg_launch_us": top["avg_us"]}
         e2e_gbs = value * 1e6 * E2E_BYTES_PER_PIXEL / 1e9
         out = {
-            "metric": METRIC_SHAPE if SHAPE else METRIC_NC if NC else METRIC, "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world,
+            "metric": METRIC_SHAPE if SHAPE else METRIC_NC if NC else METRIC.format(S=S), "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (msegment.synth %s, splitmix64; regenerated on the box)" % args.kind,
@@ -490,6 +593,7 @@ def main(argv=None):
             "roofline": roof,
             "colour_distance": stencil,
             "batch": batch,
+            "stress": stress,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
             "e2e_hbm": {"achieved": round(e2e_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -506,4 +610,4 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

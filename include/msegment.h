@@ -114,9 +114,16 @@ int msg_watershed_batch(msg_ctx* ctx, int n, const uint8_t* const* bgr, const si
 /* Floods kept in flight by the batch entry points (1..8, default 4; 1 = back to back). */
 int msg_set_batch_inflight(msg_ctx* ctx, int k);
 
+/* Blocks per launch of the flood's decision kernel (0 = default: one wave of the device's
+ * occupancy).  A performance knob only: its rank chunks are dealt in dispatch order, so any
+ * grid size -- and any number of concurrent floods -- makes progress. */
+int msg_set_resolve_grid(msg_ctx* ctx, int blocks);
+
 /* ---- device-resident entry points (dense layouts; pointers are device memory of the
- * context's device; stream = hipStream_t or NULL for the context's own stream).  They return
- * when the flood has finished; the colourise kernel may still be in flight on `stream`. ---- */
+ * context's device; stream = hipStream_t, or NULL: the work then runs on the context's own
+ * stream, ordered after what the legacy null stream had queued and before what it queues
+ * next, i.e. as if on the null stream).  They return when the flood has finished; the
+ * colourise kernel may still be in flight on `stream`. ---- */
 
 /* d_markers_in (int32) is read, d_labels (int32) written; they may alias (in place). */
 int msg_watershed_dev(msg_ctx* ctx, const void* d_bgr, const void* d_markers_in, void* d_labels,

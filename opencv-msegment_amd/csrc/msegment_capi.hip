@@ -55,9 +55,11 @@ struct msg_ctx {
   // host-mapped progress mirror {iteration, done, error, remaining}, written by k_scatter
   int* h_mir = nullptr;
   int* d_mir = nullptr;  // its device address
+  // ordering with the legacy null stream for device calls given stream = NULL (StreamScope)
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
   unsigned epoch = 1;
   int group = 8;
-  int res_grid = 0;   // co-resident k_resolve blocks (occupancy x CUs), bounded-spin safety
+  int res_grid = 0;   // k_resolve blocks per launch (occupancy x CUs by default; a perf knob)
   msg_stats stats{};
   // optional per-kernel HIP-event profiling (msg_set_profiling)
   bool prof = false;
@@ -157,6 +159,28 @@ int fail(msg_ctx* c, int code, const char* fmt, ...) {
       return fail((c), e_ == hipErrorOutOfMemory ? MSG_ENOMEM : MSG_EHIP, "%s: %s (%s:%d)", \
                   #call, hipGetErrorString(e_), __FILE__, __LINE__);                         \
   } while (0)
+
+// Device entry points with stream == NULL run on the context's own non-blocking stream, which
+// does not order with the legacy null stream that e.g. torch's default stream is.  The scope
+// makes the own stream wait for the null stream's work on entry, and the null stream wait for
+// the own stream's work on exit, so stream = NULL behaves like the caller's default stream.
+struct StreamScope {
+  msg_ctx* c;
+  hipStream_t st;
+  int rc = MSG_OK;
+  bool joined = false;
+  StreamScope(msg_ctx* c_, void* stream) : c(c_), st(stream ? (hipStream_t)stream : c_->own) {
+    if (stream) return;
+    if (hipEventRecord(c->ev_in, nullptr) != hipSuccess || hipStreamWaitEvent(c->own, c->ev_in, 0) != hipSuccess)
+      rc = fail(c, MSG_EHIP, "cannot order the context stream after the null stream");
+    else
+      joined = true;
+  }
+  ~StreamScope() {
+    if (!joined) return;
+    if (hipEventRecord(c->ev_out, c->own) == hipSuccess) (void)hipStreamWaitEvent(nullptr, c->ev_out, 0);
+  }
+};
 
 template <class T>
 void dfree(T*& p) {
@@ -388,13 +412,6 @@ int upload_palette(msg_ctx* c, const uint8_t* pal, int depth, hipStream_t st) {
 
 constexpr int MAX_INFLIGHT = 8;
 
-// Hardware queues per process of the HIP runtime (GPU_MAX_HW_QUEUES, default 4).
-int hw_queues() {
-  const char* e = getenv("GPU_MAX_HW_QUEUES");
-  const int q = e ? atoi(e) : 0;
-  return q > 0 ? q : 4;
-}
-
 int ensure_subs(msg_ctx* c, int k) {
   while ((int)c->subs.size() < k) {
     msg_ctx* sub = nullptr;
@@ -433,11 +450,9 @@ int run_batch(msg_ctx* c, int n, F fn) {
   int rc = ensure_subs(c, k);
   if (rc) return rc;
   // up to min(k, hardware queues) floods run kernels concurrently (streams beyond the HIP
-  // runtime's hardware queues share them and serialise): k_resolve's waits on lower ranks are
-  // only safe while every block of every concurrent k_resolve grid can be resident at once, so
-  // the co-resident budget (occupancy x CUs) is split between the concurrent floods
-  const int conc = std::max(1, std::min(k, hw_queues()));
-  for (int w = 0; w < k; ++w) c->subs[w]->res_grid = std::max(1, c->res_grid / conc);
+  // runtime's hardware queues share them and serialise).  k_resolve deals its rank chunks in
+  // dispatch order, so concurrent grids need not be co-resident: each keeps the full grid.
+  for (int w = 0; w < k; ++w) c->subs[w]->res_grid = c->res_grid;
   std::vector<int> rcs(k, MSG_OK);
   std::vector<msg_stats> st(k);
   std::vector<std::thread> th;
@@ -588,7 +603,9 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
       hipMalloc((void**)&c->d_ctl, sizeof(Ctl)) != hipSuccess ||
       hipHostMalloc((void**)&c->h_mir, 4 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
-      hipHostGetDevicePointer((void**)&c->d_mir, c->h_mir, 0) != hipSuccess) {
+      hipHostGetDevicePointer((void**)&c->d_mir, c->h_mir, 0) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming) != hipSuccess) {
     msg_destroy(c);
     return MSG_EHIP;
   }
@@ -600,8 +617,9 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
       msg_destroy(c);
       return MSG_EHIP;
     }
-    // blocks of a k_resolve round wait on each other, so the grid must be co-resident: the
-    // occupancy answer (3 x 512 threads per CU at k_resolve's 80 VGPRs), capped at 4
+    // one full wave of k_resolve blocks (3 x 512 threads per CU at its 80 VGPRs, capped at 4):
+    // a performance choice only -- chunks are dealt in dispatch order, so progress does not
+    // depend on how many of the blocks are resident (msg_set_resolve_grid overrides it)
     c->res_grid = cus * std::max(1, std::min(per, 4));
     c->cus = cus;
   }
@@ -631,6 +649,8 @@ void msg_destroy(msg_ctx* c) {
   if (c->h_hist) (void)hipHostFree(c->h_hist);
   if (c->h_mir) (void)hipHostFree(c->h_mir);
   for (auto& e : c->evpool) (void)hipEventDestroy(e);
+  if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+  if (c->ev_out) (void)hipEventDestroy(c->ev_out);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
 }
@@ -690,7 +710,9 @@ int msg_watershed_dev(msg_ctx* c, const void* d_bgr, const void* d_markers_in, v
   if ((long long)rows * cols > 0 && (!d_bgr || !d_markers_in || !d_labels))
     return fail(c, MSG_EINVAL, "null device pointer");
   HIPCHK(c, hipSetDevice(c->dev));
-  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  StreamScope scope(c, stream);
+  if (scope.rc) return scope.rc;
+  hipStream_t st = scope.st;
   return run_flood(c, (const uint8_t*)d_bgr, (const int32_t*)d_markers_in, (int32_t*)d_labels,
                    rows, cols, st);
 }
@@ -704,7 +726,9 @@ int msg_colorize_dev(msg_ctx* c, const void* d_labels, int rows, int cols, int d
   if ((long long)rows * cols > 0 && (!d_labels || !d_dst_bgr))
     return fail(c, MSG_EINVAL, "null device pointer");
   HIPCHK(c, hipSetDevice(c->dev));
-  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  StreamScope scope(c, stream);
+  if (scope.rc) return scope.rc;
+  hipStream_t st = scope.st;
   return launch_colorize(c, (const int32_t*)d_labels, (long long)rows * cols, depth,
                          (const uint8_t*)d_palette_bgr, (uint8_t*)d_dst_bgr, (uint8_t*)d_gray, st);
 }
@@ -720,7 +744,9 @@ int msg_watershed_colorize_dev(msg_ctx* c, const void* d_bgr, const void* d_mark
   if ((long long)rows * cols > 0 && (!d_bgr || !d_markers_in || !d_labels || !d_dst_bgr))
     return fail(c, MSG_EINVAL, "null device pointer");
   HIPCHK(c, hipSetDevice(c->dev));
-  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  StreamScope scope(c, stream);
+  if (scope.rc) return scope.rc;
+  hipStream_t st = scope.st;
   return run_flood(c, (const uint8_t*)d_bgr, (const int32_t*)d_markers_in, (int32_t*)d_labels, rows,
                    cols, st, depth, (const uint8_t*)d_palette_bgr, (uint8_t*)d_dst_bgr,
                    (uint8_t*)d_gray);
@@ -735,7 +761,9 @@ int msg_edge_weights_dev(msg_ctx* c, const void* d_bgr, void* d_wright, void* d_
   if (N == 0) return MSG_OK;
   if (!d_bgr || !d_wright || !d_wdown) return fail(c, MSG_EINVAL, "null device pointer");
   HIPCHK(c, hipSetDevice(c->dev));
-  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  StreamScope scope(c, stream);
+  if (scope.rc) return scope.rc;
+  hipStream_t st = scope.st;
   const bool vec = cols % 16 == 0 && (((uintptr_t)d_bgr | (uintptr_t)d_wright | (uintptr_t)d_wdown) & 15) == 0;
   if (vec) {
     if (N <= (8ll << 20) * 4) {  // up to 2 x 4096^2 pixels: 2 rows per thread (ws_kernels.hip)
@@ -802,22 +830,11 @@ int msg_watershed_colorize(msg_ctx* c, const uint8_t* bgr, size_t bgr_stride, in
   if (rc) return rc;
   HIPCHK(c, hipMemcpy2DAsync(markers, marker_stride, c->d_mk, (size_t)cols * 4, (size_t)cols * 4,
                              rows, hipMemcpyDeviceToHost, st));
-  // read-back guard: cv::watershed leaves the whole first row at WSHED.  (An all-zero frame was
-  // once returned here: the workspace's zero fill ran as a null-stream hipMemset, unordered with
-  // the flood stream -- fixed in ensure_flood; the check stays as a cheap consistency test.)
-  auto row0_ok = [&]() {
-    for (int j = 0; j < cols; ++j)
-      if (markers[j] != WSHED) return false;
-    return true;
-  };
+  // consistency check, no retry: cv::watershed leaves the whole first row at WSHED, so anything
+  // else means the flood or the read-back was misordered -- a hard error, never re-issued
   HIPCHK(c, hipStreamSynchronize(st));
-  if (!row0_ok()) {
-    HIPCHK(c, hipMemcpy2DAsync(markers, marker_stride, c->d_mk, (size_t)cols * 4, (size_t)cols * 4, rows,
-                               hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipStreamSynchronize(st));
-    if (!row0_ok()) return fail(c, MSG_ESTATE, "label read-back failed the frame-border check");
-    std::fprintf(stderr, "libmsegment: label read-back re-issued (frame-border check)\n");
-  }
+  for (int j = 0; j < cols; ++j)
+    if (markers[j] != WSHED) return fail(c, MSG_ESTATE, "label read-back failed the frame-border check");
   if (want_color) {
     HIPCHK(c, hipMemcpy2DAsync(dst_bgr, dst_stride, c->d_dst, (size_t)cols * 3, (size_t)cols * 3,
                                rows, hipMemcpyDeviceToHost, st));
@@ -877,6 +894,19 @@ int msg_watershed_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size
   });
 }
 
+int msg_set_resolve_grid(msg_ctx* c, int blocks) {
+  if (!c || blocks < 0) return MSG_EINVAL;
+  if (blocks == 0) {
+    int per = 0;
+    HIPCHK(c, hipSetDevice(c->dev));
+    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_resolve, RBS, 0));
+    blocks = c->cus * std::max(1, std::min(per, 4));
+  }
+  c->res_grid = blocks;
+  for (msg_ctx* sub : c->subs) sub->res_grid = blocks;
+  return MSG_OK;
+}
+
 int msg_set_batch_inflight(msg_ctx* c, int k) {
   if (!c || k < 1) return MSG_EINVAL;
   c->inflight = std::min(k, MAX_INFLIGHT);
@@ -910,7 +940,9 @@ int msg_gray_hist_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, void* d
   if (!aligned(d_bgr, 4) || !aligned(d_gray, 4))
     return fail(c, MSG_EINVAL, "d_bgr and d_gray must be 4-byte aligned");
   HIPCHK(c, hipSetDevice(c->dev));
-  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  StreamScope scope(c, stream);
+  if (scope.rc) return scope.rc;
+  hipStream_t st = scope.st;
   return gray_hist(c, (const uint8_t*)d_bgr, N, (uint8_t*)d_gray, hist256, st);
 }
 
@@ -925,7 +957,9 @@ int msg_nc_markers_dev(msg_ctx* c, const void* d_gray, int rows, int cols, const
   if (!aligned(d_gray, 4) || !aligned(d_markers, 16))
     return fail(c, MSG_EINVAL, "d_gray must be 4-byte and d_markers 16-byte aligned");
   HIPCHK(c, hipSetDevice(c->dev));
-  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  StreamScope scope(c, stream);
+  if (scope.rc) return scope.rc;
+  hipStream_t st = scope.st;
   return nc_markers(c, (const uint8_t*)d_gray, N, lut256, (int32_t*)d_markers, st);
 }
 
@@ -944,7 +978,9 @@ int msg_nc_marker_stage_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, i
   if (!aligned(d_bgr, 4) || !aligned(d_gray, 4) || !aligned(d_markers, 16))
     return fail(c, MSG_EINVAL, "d_bgr/d_gray must be 4-byte and d_markers 16-byte aligned");
   HIPCHK(c, hipSetDevice(c->dev));
-  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  StreamScope scope(c, stream);
+  if (scope.rc) return scope.rc;
+  hipStream_t st = scope.st;
   uint8_t* g = (uint8_t*)d_gray;
   if (!g && N > 0) {
     if (c->gscr_n < N) {
@@ -1017,7 +1053,9 @@ int msg_shape_markers_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, int
   const int k = ksize > 0 ? ksize : blur_mask_size(rows, cols);
   if (k % 2 == 0 || k > 255) return fail(c, MSG_EINVAL, "median size %d: odd and <= 255", k);
   HIPCHK(c, hipSetDevice(c->dev));
-  hipStream_t st = stream ? (hipStream_t)stream : c->own;
+  StreamScope scope(c, stream);
+  if (scope.rc) return scope.rc;
+  hipStream_t st = scope.st;
   const int H = rows, W = cols;
   const long long nb = (long long)((H + 1) >> 1) * ((W + 1) >> 1);
   rc = ensure_shape(c, N, nb);

@@ -825,9 +825,10 @@ __device__ __forceinline__ bool attempt_item(const Item& it, F fetch, int& lab_o
 // k_resolve: label of an item = fold of its settled neighbours and of the labels of EARLIER batch
 // items adjacent to it; it pushes a 0-neighbour z unless an earlier batch item adjacent to z has
 // a non-WSHED label (serially that item pushed z first).  Both only wait on LOWER ranks.  Ranks
-// are dealt round-robin over the co-resident grid (block-round r covers ranks
-// [r*G*RBS, (r+1)*G*RBS)), so a lower rank is in the same round or an earlier one: bounded
-// spinning cannot deadlock.  In-wave dependencies go through register shuffles, others through
+// are dealt in chunks of RBS from an atomic dispenser in dispatch order (a block takes its next
+// chunk when it starts the current one), so every lower rank belongs to a chunk that a block
+// which is already running holds: the lowest unfinished chunk always has everything it waits on
+// finished, whatever the grid size and however many blocks are resident.  In-wave dependencies go through register shuffles, others through
 // 8-byte granules {epoch, label} (final) or {epoch | bit 63, base fold} (provisional: a pending
 // dep whose settled neighbours fold to b can only end as b or WSHED).  Items then add their
 // pushes to the per-chunk level histograms and the cut words, which k_scan consumes.
@@ -848,9 +849,19 @@ __global__ __launch_bounds__(RBS, 6) void k_resolve(Ws ws) {
   const unsigned long long etag = (unsigned long long)B.epoch << 32;  // final label granule
   const unsigned long long ptag = etag | (1ull << 63);                // provisional base fold
   unsigned long long* const dg = ws.diag;
-  for (int base = blockIdx.x * RBS; work && base < B.n; base += gridDim.x * RBS) {
+  __shared__ int s_chunk, s_next;
+  if (tid == 0 && work) s_next = (int)atomicAdd(&ctl->rticket, 1u);
+  for (;;) {
+    if (!work) break;
+    if (tid == 0) {
+      s_chunk = s_next;
+      // the next chunk is claimed now, so its dispenser round trip overlaps this chunk's work
+      if ((long long)s_chunk * RBS < B.n) s_next = (int)atomicAdd(&ctl->rticket, 1u);
+    }
     if (tid < NQ) hist[tid] = 0;
     __syncthreads();
+    const int base = s_chunk * RBS;
+    if (base >= B.n) break;
     const int wbase = base + (tid & ~63);
     const int i = wbase + lane;
     const bool valid = i < B.n;
@@ -1041,6 +1052,7 @@ __global__ __launch_bounds__(RBS, 6) void k_resolve(Ws ws) {
 // following small batches itself (small_loop).
 __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
   Ctl* ctl = ws.ctl;
+  if (threadIdx.x == 0) ctl->rticket = 0;  // this iteration's k_resolve has finished
   const Batch cb = scan_body(ws);
   if (cb.nchunk > 0 && cb.n <= SMALL_MAX && !ctl->error) {
     scatter_chunks(ws, cb, 0, 1);

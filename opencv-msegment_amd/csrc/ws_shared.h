@@ -98,6 +98,7 @@ struct Ctl {
   int done;
   int error;
   int remaining;  // queued items after the last batch was formed (host polling hint)
+  unsigned rticket;  // k_resolve's rank-chunk dispenser (dispatch order), reset by k_scan
   long long batches;
   long long pops;
   long long items;   // sum of batch sizes resolved (committed or not)

@@ -1,13 +1,45 @@
 // msegment_jni.cpp -- JNI shim over the C ABI of include/msegment.h.
-// Build (where a JDK exists):
-//   g++ -O2 -fPIC -shared -I"$JAVA_HOME/include" -I"$JAVA_HOME/include/linux" -I../../include \
+// Build (where a JDK exists), one command:
+//   g++ -O2 -fPIC -shared -I"$JAVA_HOME/include" -I"$JAVA_HOME/include/linux" -I../../include
 //       msegment_jni.cpp -L../msegment -lmsegment -Wl,-rpath,'$ORIGIN' -o libmsegment_jni.so
 // Replaces the OpenCV 3.4.2 JNI entry Java_org_opencv_imgproc_Imgproc_watershed_10 reached from
 // PictureService.java:909, plus the per-pixel colorByIndexes loop (PictureService.java:913-936),
-// and the marker stage of notConnectedMarkers (PictureService.java:476-828).
+// and the marker stages of notConnectedMarkers (PictureService.java:476-828) and
+// shapeAutoMarkerWatershed (PictureService.java:402-452).
+//
+// Every Java array is checked against the sizes rows/cols/depth imply before anything is read
+// (a short array returns MSG_EINVAL instead of letting libmsegment run past it), and the arrays
+// are copied with Get/Set<Type>ArrayRegion into native buffers: no critical region is held while
+// the GPU works (the flood can take seconds on interrupt-dense frames, and a critical region
+// blocks the garbage collector for that long).  tests/test_jni_shim.py compiles this file against
+// a JNI type stub and drives it through a mock JNIEnv.
 #include <jni.h>
 
+#include <cstdint>
+#include <new>
+#include <vector>
+
 #include "msegment.h"
+
+namespace {
+
+// rows * cols * k fits the Java array of length `len` (and is representable)
+bool fits(JNIEnv* env, jarray a, jint rows, jint cols, long long k) {
+  if (!a || rows < 0 || cols < 0) return false;
+  return (long long)env->GetArrayLength(a) >= (long long)rows * cols * k;
+}
+
+template <class T>
+bool alloc(std::vector<T>& v, long long n) {
+  try {
+    v.resize((size_t)n);
+  } catch (const std::bad_alloc&) {
+    return false;
+  }
+  return true;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -27,27 +59,32 @@ JNIEXPORT jstring JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNa
   return env->NewStringUTF(msg_last_error(reinterpret_cast<msg_ctx*>(ctx)));
 }
 
+// PictureService.watershed (PictureService.java:908-911): markers rewritten in place (labels),
+// dst = colorByIndexes(markers, depth, palette != null).
 JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_watershedColorize(
     JNIEnv* env, jclass, jlong ctx, jbyteArray bgr, jintArray markers, jint rows, jint cols, jint depth,
     jbyteArray palette, jbyteArray dst) {
   msg_ctx* c = reinterpret_cast<msg_ctx*>(ctx);
-  if (!c) return MSG_EINVAL;
-  // pinned (critical) views: no per-pixel JNI traffic, one H2D/D2H per buffer inside libmsegment
-  jbyte* pb = static_cast<jbyte*>(env->GetPrimitiveArrayCritical(bgr, nullptr));
-  jint* pm = static_cast<jint*>(env->GetPrimitiveArrayCritical(markers, nullptr));
-  jbyte* pd = static_cast<jbyte*>(env->GetPrimitiveArrayCritical(dst, nullptr));
-  jbyte* pp = palette ? static_cast<jbyte*>(env->GetPrimitiveArrayCritical(palette, nullptr)) : nullptr;
-  int rc = MSG_EINVAL;
-  if (pb && pm && pd)
-    rc = msg_watershed_colorize(c, reinterpret_cast<const uint8_t*>(pb), (size_t)cols * 3,
-                                reinterpret_cast<int32_t*>(pm), (size_t)cols * 4, rows, cols, depth,
-                                reinterpret_cast<const uint8_t*>(pp), reinterpret_cast<uint8_t*>(pd),
-                                (size_t)cols * 3, nullptr, 0);
-  if (pp) env->ReleasePrimitiveArrayCritical(palette, pp, JNI_ABORT);
-  if (pd) env->ReleasePrimitiveArrayCritical(dst, pd, 0);
-  if (pm) env->ReleasePrimitiveArrayCritical(markers, pm, 0);
-  if (pb) env->ReleasePrimitiveArrayCritical(bgr, pb, JNI_ABORT);
-  return rc;
+  if (!c || depth < 0 || !fits(env, bgr, rows, cols, 3) || !fits(env, markers, rows, cols, 1) ||
+      !fits(env, dst, rows, cols, 3) || (palette && env->GetArrayLength(palette) < 3ll * depth))
+    return MSG_EINVAL;
+  const long long n = (long long)rows * cols;
+  std::vector<jbyte> b, d, p;
+  std::vector<jint> m;
+  if (!alloc(b, 3 * n) || !alloc(m, n) || !alloc(d, 3 * n) || (palette && !alloc(p, 3ll * depth)))
+    return MSG_ENOMEM;
+  env->GetByteArrayRegion(bgr, 0, (jsize)(3 * n), b.data());
+  env->GetIntArrayRegion(markers, 0, (jsize)n, m.data());
+  if (palette) env->GetByteArrayRegion(palette, 0, 3 * depth, p.data());
+  if (env->ExceptionCheck()) return MSG_EINVAL;
+  const int rc = msg_watershed_colorize(c, reinterpret_cast<const uint8_t*>(b.data()), (size_t)cols * 3,
+                                        reinterpret_cast<int32_t*>(m.data()), (size_t)cols * 4, rows, cols,
+                                        depth, palette ? reinterpret_cast<const uint8_t*>(p.data()) : nullptr,
+                                        reinterpret_cast<uint8_t*>(d.data()), (size_t)cols * 3, nullptr, 0);
+  if (rc) return rc;
+  env->SetIntArrayRegion(markers, 0, (jsize)n, m.data());
+  env->SetByteArrayRegion(dst, 0, (jsize)(3 * n), d.data());
+  return MSG_OK;
 }
 
 // notConnectedMarkers' marker stage (PictureService.java:476-828): markers out, levels as
@@ -57,27 +94,30 @@ JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNativ
     JNIEnv* env, jclass, jlong ctx, jbyteArray bgr, jint rows, jint cols, jint depth, jint options,
     jintArray markers, jintArray levelsOut) {
   msg_ctx* c = reinterpret_cast<msg_ctx*>(ctx);
-  if (!c || env->GetArrayLength(levelsOut) < 3 * 256) return MSG_EINVAL;
+  if (!c || !levelsOut || env->GetArrayLength(levelsOut) < 3 * 256 || !fits(env, bgr, rows, cols, 3) ||
+      !fits(env, markers, rows, cols, 1))
+    return MSG_EINVAL;
+  const long long n = (long long)rows * cols;
+  std::vector<jbyte> b;
+  std::vector<jint> m;
+  if (!alloc(b, 3 * n) || !alloc(m, n)) return MSG_ENOMEM;
+  env->GetByteArrayRegion(bgr, 0, (jsize)(3 * n), b.data());
+  if (env->ExceptionCheck()) return MSG_EINVAL;
   msg_bright_level lv[256];
-  int n = 0;
-  jbyte* pb = static_cast<jbyte*>(env->GetPrimitiveArrayCritical(bgr, nullptr));
-  jint* pm = static_cast<jint*>(env->GetPrimitiveArrayCritical(markers, nullptr));
-  int rc = MSG_EINVAL;
-  if (pb && pm)
-    rc = msg_nc_marker_stage(c, reinterpret_cast<const uint8_t*>(pb), (size_t)cols * 3, rows, cols,
-                             depth, (unsigned)options, reinterpret_cast<int32_t*>(pm),
-                             (size_t)cols * 4, lv, 256, &n);
-  if (pm) env->ReleasePrimitiveArrayCritical(markers, pm, 0);
-  if (pb) env->ReleasePrimitiveArrayCritical(bgr, pb, JNI_ABORT);
+  int nl = 0;
+  const int rc = msg_nc_marker_stage(c, reinterpret_cast<const uint8_t*>(b.data()), (size_t)cols * 3, rows,
+                                     cols, depth, (unsigned)options, reinterpret_cast<int32_t*>(m.data()),
+                                     (size_t)cols * 4, lv, 256, &nl);
   if (rc) return rc;
   jint tri[3 * 256];
-  for (int i = 0; i < n; ++i) {
+  for (int i = 0; i < nl; ++i) {
     tri[3 * i] = lv[i].start;
     tri[3 * i + 1] = lv[i].end;
     tri[3 * i + 2] = lv[i].count;
   }
-  env->SetIntArrayRegion(levelsOut, 0, 3 * n, tri);
-  return n;
+  env->SetIntArrayRegion(markers, 0, (jsize)n, m.data());
+  env->SetIntArrayRegion(levelsOut, 0, 3 * nl, tri);
+  return nl;
 }
 
 // shapeAutoMarkerWatershed's marker stage (PictureService.java:402-452): markers out (the
@@ -86,17 +126,19 @@ JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNativ
 JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_shapeMarkers(
     JNIEnv* env, jclass, jlong ctx, jbyteArray bgr, jint rows, jint cols, jintArray markers) {
   msg_ctx* c = reinterpret_cast<msg_ctx*>(ctx);
-  if (!c) return MSG_EINVAL;
+  if (!c || !fits(env, bgr, rows, cols, 3) || !fits(env, markers, rows, cols, 1)) return MSG_EINVAL;
+  const long long n = (long long)rows * cols;
+  std::vector<jbyte> b;
+  std::vector<jint> m;
+  if (!alloc(b, 3 * n) || !alloc(m, n)) return MSG_ENOMEM;
+  env->GetByteArrayRegion(bgr, 0, (jsize)(3 * n), b.data());
+  if (env->ExceptionCheck()) return MSG_EINVAL;
   int depth = 0, ncomp = 0;
-  jbyte* pb = static_cast<jbyte*>(env->GetPrimitiveArrayCritical(bgr, nullptr));
-  jint* pm = static_cast<jint*>(env->GetPrimitiveArrayCritical(markers, nullptr));
-  int rc = MSG_EINVAL;
-  if (pb && pm)
-    rc = msg_shape_markers(c, reinterpret_cast<const uint8_t*>(pb), (size_t)cols * 3, rows, cols, 0,
-                           reinterpret_cast<int32_t*>(pm), (size_t)cols * 4, &depth, &ncomp);
-  if (pm) env->ReleasePrimitiveArrayCritical(markers, pm, 0);
-  if (pb) env->ReleasePrimitiveArrayCritical(bgr, pb, JNI_ABORT);
-  return rc ? rc : depth;
+  const int rc = msg_shape_markers(c, reinterpret_cast<const uint8_t*>(b.data()), (size_t)cols * 3, rows, cols,
+                                   0, reinterpret_cast<int32_t*>(m.data()), (size_t)cols * 4, &depth, &ncomp);
+  if (rc) return rc;
+  env->SetIntArrayRegion(markers, 0, (jsize)n, m.data());
+  return depth;
 }
 
 }  // extern "C"

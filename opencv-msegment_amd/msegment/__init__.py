@@ -201,6 +201,10 @@ class Segmenter:
         """Floods kept in flight by the batch calls (1..8; 1 = back to back)."""
         self._check(self._L.msg_set_batch_inflight(self._h, int(k)))
 
+    def set_resolve_grid(self, blocks=0):
+        """Blocks per k_resolve launch (0 = the default); a performance knob only."""
+        self._check(self._L.msg_set_resolve_grid(self._h, int(blocks)))
+
     # -- device-resident buffers (torch tensors on this device) ---------------------------
     @staticmethod
     def _stream(stream):

@@ -30,7 +30,7 @@ EXPORTS = (
     "msg_watershed", "msg_colorize", "msg_watershed_colorize", "msg_watershed_batch",
     "msg_watershed_dev", "msg_colorize_dev", "msg_watershed_colorize_dev", "msg_edge_weights_dev",
     "msg_set_profiling", "msg_get_kernel_profile", "msg_set_diag",
-    "msg_set_batch_inflight", "msg_watershed_colorize_batch_dev",
+    "msg_set_batch_inflight", "msg_set_resolve_grid", "msg_watershed_colorize_batch_dev",
     "msg_gray_hist_dev", "msg_nc_levels", "msg_nc_marker_lut", "msg_nc_markers_dev",
     "msg_nc_marker_stage_dev", "msg_nc_marker_stage",
     "msg_blur_mask_size", "msg_shape_markers_dev", "msg_shape_markers",
@@ -125,6 +125,8 @@ def load():
     L.msg_get_kernel_profile.restype = i
     L.msg_set_batch_inflight.argtypes = [vp, i]
     L.msg_set_batch_inflight.restype = i
+    L.msg_set_resolve_grid.argtypes = [vp, i]
+    L.msg_set_resolve_grid.restype = i
     L.msg_watershed_colorize_batch_dev.argtypes = [vp, i, vp, vp, vp, vp, vp, i, vp, vp, vp]
     L.msg_watershed_colorize_batch_dev.restype = i
     L.msg_gray_hist_dev.argtypes = [vp, vp, i, i, vp, vp, vp]

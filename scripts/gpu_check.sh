@@ -25,7 +25,7 @@ if [ -z "${PROF_ONLY:-}" ]; then
 fi
 # the profiled command is the headline's single-flood path only (--batch-frames 1: no concurrent
 # floods, whose overlapping kernels would inflate the per-launch durations and traffic)
-PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass --batch-frames 1"
+PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass --batch-frames 1 --stress-steps 0"
 run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py $PROF_ARGS
 find "$OUT/prof" -name '*stats*' -exec cp {} "$OUT/" \; 2>/dev/null
 # HBM traffic: one counter group per rocprofv3 run, kernel trace only (MI355X_MICROARCH.md)

@@ -4,7 +4,10 @@ per launch.  FETCH_SIZE is doubled: on gfx950 it reports half the bytes of wide 
 (MI355X_MICROARCH.md, HBM/rocprofv3 section; checked here on k_untile, whose 16-B-per-lane loads
 move a known 8 B per pixel).  Other read widths (random 4-8 B gathers) are uncalibrated.
 
-  python scripts/pmc_summary.py <dir with pmc_FETCH_SIZE/ and pmc_WRITE_SIZE/> <out.json> [note]
+  python scripts/pmc_summary.py <dir with pmc_FETCH_SIZE/ and pmc_WRITE_SIZE/> <out.json> [note] [bench args]
+
+The workload of the profiled command (bench.py's defaults unless bench args are given) is stored
+as "config"; bench.py quotes the traffic only for that same workload.
 """
 import re
 import collections
@@ -28,6 +31,19 @@ def load(path, counter):
     return {k: (tot[k], n[k]) for k in tot}
 
 
+def bench_config(argv):
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pipeline", default="watershed")
+    ap.add_argument("--kind", default="mosaic")
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--frames", type=int, default=1)
+    a, _ = ap.parse_known_args(argv)
+    return {"pipeline": a.pipeline, "kind": a.kind, "size": a.size, "seed": a.seed, "frames": a.frames}
+
+
 def main():
     src, out = sys.argv[1], sys.argv[2]
     fetch = load(os.path.join(src, "pmc_FETCH_SIZE"), "FETCH_SIZE")
@@ -43,7 +59,7 @@ def main():
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs) of "
                      "`python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass --batch-frames 1`",
            "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes", "note": sys.argv[3] if len(sys.argv) > 3 else "",
-           "kernels": res}
+           "config": bench_config(sys.argv[4:]), "kernels": res}
     json.dump(doc, open(out, "w"), indent=1)
     for k, v in res.items():
         print("%-12s launches %6d  fetch %10.0f  write %10.0f  B/launch" % (k, v["launches"], v["fetch_bytes_per_launch"], v["write_bytes_per_launch"]))

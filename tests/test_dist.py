@@ -67,3 +67,31 @@ def test_whole_job_value_is_sum_over_ranks():
 
     assert bench.whole_job_mpx(world=4, npx=4096 * 4096, steps=10, dt_max=2.0) == pytest.approx(
         4 * 4096 * 4096 * 10 / 2.0 / 1e6)
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`python bench.py --gpus 2` with no launcher starts 2 ranks itself (torch.distributed.run
+    children, before any GPU call) and rank 0 reports n_gpus = 2.  The harness-test step (a sleep,
+    gloo) stands in for the GPU step so the launch path runs on CPU."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, MSEG_BENCH_HARNESS_TEST="1", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+                          "--warmup", "1"], env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1                     # rank 0 only
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["steps"] == 3
+    assert d["value"] == pytest.approx(2 * 3 / (d["ms_per_step"] * 3 / 1000.0), rel=1e-3)
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    import subprocess
+
+    env = dict(os.environ, MSEG_BENCH_HARNESS_TEST="1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr

@@ -118,6 +118,19 @@ def test_config3_4096_mosaic_digest_and_properties(seg):
     check_properties(m, out)
 
 
+@pytest.mark.parametrize("kind", ["mosaic_noise", "random"])
+def test_config3_4096_stress_digest_and_properties(seg, kind):
+    """BASELINE config 3's stress variants (mosaic+noise, uniform-random; 4096^2, seed 2): the
+    interrupt-dense regime at full size, against the oracle's digest, plus the invariants."""
+    key = "%s_4096x4096_s2" % kind
+    dg = json.load(open(os.path.join(GOLD, "digests.json")))[key]
+    img, m, d = synth.frame(kind, 4096, 4096, 2)
+    out = gpu_ws(seg, img, m)
+    assert hashlib.sha256(out.tobytes()).hexdigest() == dg["labels_sha256"]
+    assert int((out == -1).sum()) == dg["wshed_pixels"]
+    check_properties(m, out)
+
+
 def test_config4_16384_mosaic_digest_single_gpu(seg):
     """BASELINE config 4's frame (16384^2, SURVEY.md seed 3) on ONE GPU: the 2^28-pixel frame's
     ~12 GB workspace fits one MI355X (why it is not tile-sharded)."""
@@ -324,10 +337,10 @@ def test_picture_service_mirror(seg):
 
 def test_batch_inflight_more_hw_queues():
     """Regression: with more hardware queues than the default 4, 8 concurrent 4096^2 floods used
-    to time out in k_resolve's cross-rank waits (their grids were not all co-resident); run_batch
-    now splits the co-resident budget between min(inflight, GPU_MAX_HW_QUEUES) floods.  Runs in a
-    child process (the queue count is fixed when HIP initialises); labels must equal the same
-    frames flooded one at a time."""
+    to time out in k_resolve's cross-rank waits (their grids were not all co-resident).  k_resolve
+    now deals rank chunks in dispatch order, and every flood keeps the full grid (no budget
+    split).  Runs in a child process (the queue count is fixed when HIP initialises); labels must
+    equal the same frames flooded one at a time."""
     import subprocess
     import sys
 
@@ -370,3 +383,78 @@ def test_c_abi_error_paths(seg):
     assert np.array_equal(out, ws_oracle.watershed(img, mk))
     # empty frames are a no-op, not an error
     assert L.msg_watershed(h, ip, 24, mp, 32, 0, 8) == 0
+
+
+@pytest.mark.parametrize("blocks", [1, 7, 16 * 256 * 4])
+def test_resolve_grid_any_size(seg, blocks):
+    """k_resolve's progress does not depend on co-residency: one block, a few, and a grid 16x
+    larger than the device can hold all give the oracle's labels without MSG_ETIMEOUT."""
+    img, m, d = synth.frame("mosaic", 1024, 1024, 1)
+    dg = json.load(open(os.path.join(GOLD, "digests.json")))["mosaic_1024x1024_s1"]
+    seg.set_resolve_grid(blocks)
+    try:
+        out = gpu_ws(seg, img, m)
+    finally:
+        seg.set_resolve_grid(0)
+    assert hashlib.sha256(out.tobytes()).hexdigest() == dg["labels_sha256"]
+
+
+def test_two_contexts_two_threads():
+    """Two Segmenters flooding at the same time from two host threads (the one-context-per-thread
+    model of include/msegment.h), each with the full k_resolve grid: both bit-exact."""
+    import threading
+
+    import msegment
+
+    fr = [synth.frame("mosaic", 2048, 2048, 40 + k) for k in range(2)]
+    want = [ws_oracle.watershed(img, m) for img, m, _ in fr]
+    got = [None, None]
+    errs = []
+
+    def run(k):
+        try:
+            with msegment.Segmenter(0) as s:
+                for _ in range(3):
+                    got[k] = gpu_ws(s, fr[k][0], fr[k][1])
+                    if not np.array_equal(got[k], want[k]):
+                        break
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=100)
+    assert not errs, errs
+    for k in range(2):
+        assert np.array_equal(got[k], want[k]), k
+
+
+def test_default_stream_ordering_without_device_sync(seg):
+    """Device calls on torch's default (legacy null) stream: the library orders its own stream
+    after the null stream's queued work and the null stream after its own, so a chain of
+    stream-ordered torch ops and library calls needs no device-wide synchronize.  The inputs are
+    produced by a long torch kernel chain right before the call; the outputs are consumed by
+    torch ops right after it."""
+    import torch
+
+    dev = torch.device("cuda", seg.device)
+    img, m, d = synth.frame("mosaic_noise", 512, 640, 21)
+    want = ws_oracle.watershed(img, m)
+    big = torch.randn(3072, 3072, device=dev)
+    for _ in range(3):
+        t_img = torch.from_numpy(img).to(dev)
+        t_m0 = torch.from_numpy(m).to(dev)
+        x = big
+        for _ in range(4):
+            x = x @ big  # keep the null stream busy
+        t_m = t_m0 + (x[0, 0] * 0).to(torch.int32)  # markers written by the last queued kernel
+        t_lab = torch.empty_like(t_m)
+        seg.watershed_dev(t_img, t_m, t_lab)
+        dst = torch.empty((512, 640, 3), dtype=torch.uint8, device=dev)
+        seg.colorize_dev(t_lab, d, None, dst)
+        lab_copy = t_lab.clone()
+        dst_copy = dst.clone()
+        assert np.array_equal(lab_copy.cpu().numpy(), want)
+        assert np.array_equal(dst_copy.cpu().numpy(), ws_oracle.colorize(want, d, None))
