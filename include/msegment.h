@@ -80,7 +80,9 @@ int  msg_get_stats(const msg_ctx* ctx, msg_stats* out);
 int  msg_set_profiling(msg_ctx* ctx, int enable);
 int  msg_get_kernel_profile(msg_ctx* ctx, msg_kernel_profile* out, int max_entries, int reset);
 /* In-kernel cycle counters (s_memtime) for the flood kernels, reported in msg_stats.diag.
- * Diagnostics only: they add atomics to the kernels; never enabled in timed runs. */
+ * Diagnostics only: they add atomics to the kernels; never enabled in timed runs.
+ * enable == 2 also injects faults for tests: the decision kernel's odd blocks give up their
+ * first chunk of every batch once, which exercises the give-up / re-run path. */
 int  msg_set_diag(msg_ctx* ctx, int enable);
 
 /* ---- host-buffer entry points (synchronous; strides in BYTES) ---------------------------- */

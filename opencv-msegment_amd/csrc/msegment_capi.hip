@@ -42,7 +42,7 @@ struct msg_ctx {
   int32_t *d_qbuf = nullptr, *d_ilist = nullptr;
   int32_t *d_cnt = nullptr, *d_coff = nullptr, *d_tot = nullptr, *d_choff = nullptr;
   unsigned* d_capp = nullptr;  // CAP_SLOTS x NQ
-  unsigned long long *d_tl = nullptr, *d_desc = nullptr;
+  unsigned long long *d_tl = nullptr, *d_desc = nullptr, *d_cflag = nullptr;
   long long qcap = 0;
   // staging for the host-buffer entry points
   long long stage_n = 0;
@@ -65,6 +65,7 @@ struct msg_ctx {
   bool prof = false;
   unsigned long long* d_diag = nullptr;  // 8 counters when diagnostics are on
   bool diag = false;
+  int inject = 0;  // msg_set_diag(ctx, 2): k_resolve give-up injection (tests)
   std::vector<hipEvent_t> evpool;
   size_t evused = 0;
   std::vector<std::pair<int, size_t>> recs;  // (kernel id, index of the start event)
@@ -193,7 +194,7 @@ void free_flood(msg_ctx* c) {
   c->d_px = nullptr;
   dfree(c->d_qbuf); dfree(c->d_ilist);
   dfree(c->d_cnt); dfree(c->d_coff); dfree(c->d_tot); dfree(c->d_choff); dfree(c->d_capp);
-  dfree(c->d_tl); dfree(c->d_desc);
+  dfree(c->d_tl); dfree(c->d_desc); dfree(c->d_cflag);
   c->cap_n = c->cap_np = c->cap_rc = 0;
   c->qcap = 0;
 }
@@ -231,6 +232,8 @@ int ensure_flood(msg_ctx* c, int H, int W, hipStream_t st) {
   HIPCHK(c, hipMalloc((void**)&c->d_choff, rc * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_capp, (size_t)CAP_SLOTS * NQ * 4));
   HIPCHK(c, hipMemsetAsync(c->d_tl, 0, n * 8, st));
+  HIPCHK(c, hipMalloc((void**)&c->d_cflag, (size_t)(n / RBS + 2) * 16));
+  HIPCHK(c, hipMemsetAsync(c->d_cflag, 0, (size_t)(n / RBS + 2) * 16, st));
   c->epoch = 1;
   c->cap_n = n;
   c->cap_np = np;
@@ -288,6 +291,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   if (rc) return rc;
   if (c->epoch > 0x70000000u) {  // granule bit 63 flags a provisional value
     HIPCHK(c, hipMemsetAsync(c->d_tl, 0, c->cap_n * 8, st));
+    HIPCHK(c, hipMemsetAsync(c->d_cflag, 0, (size_t)(c->cap_n / RBS + 2) * 16, st));
     c->epoch = 1;
   }
   Ws ws;
@@ -306,6 +310,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   ws.tot = c->d_tot;
   ws.choff = c->d_choff;
   ws.capp = c->d_capp;
+  ws.cflag = c->d_cflag;
   ws.ctl = c->d_ctl;
   ws.diag = c->diag ? c->d_diag : nullptr;
   ws.hmir = c->d_mir;
@@ -340,7 +345,10 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   long long syncs = 0;
   for (;;) {
     for (int g = 0; g < c->group; ++g, ++it) {
-      LAUNCH(c, KID_RESOLVE, st, k_resolve, dim3(gres), dim3(RBS), 0, ws);
+      if (c->inject)  // test only: odd blocks give up their first chunk (msg_set_diag 2)
+        LAUNCH(c, KID_RESOLVE, st, k_resolve<true>, dim3(gres), dim3(RBS), 0, ws);
+      else
+        LAUNCH(c, KID_RESOLVE, st, k_resolve<false>, dim3(gres), dim3(RBS), 0, ws);
       LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);  // + small batches
       LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, it);
     }
@@ -612,7 +620,7 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
   {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_resolve, RBS, 0) != hipSuccess || cus <= 0 ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_resolve<false>, RBS, 0) != hipSuccess || cus <= 0 ||
         per <= 0) {
       msg_destroy(c);
       return MSG_EHIP;
@@ -676,6 +684,7 @@ int msg_set_diag(msg_ctx* c, int enable) {
     HIPCHK(c, hipMalloc((void**)&c->d_diag, 8 * sizeof(unsigned long long)));
   }
   c->diag = enable != 0;
+  c->inject = enable == 2;
   return MSG_OK;
 }
 
@@ -899,7 +908,7 @@ int msg_set_resolve_grid(msg_ctx* c, int blocks) {
   if (blocks == 0) {
     int per = 0;
     HIPCHK(c, hipSetDevice(c->dev));
-    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_resolve, RBS, 0));
+    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_resolve<false>, RBS, 0));
     blocks = c->cus * std::max(1, std::min(per, 4));
   }
   c->res_grid = blocks;

@@ -606,6 +606,7 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
   if (tid == 0) {
     Batch pb;
     pb.mode = 1;
+    pb.rrun = 0;
     pb.L = -1;
     pb.bstart = 0;
     pb.n = (int)M;
@@ -825,10 +826,15 @@ __device__ __forceinline__ bool attempt_item(const Item& it, F fetch, int& lab_o
 // k_resolve: label of an item = fold of its settled neighbours and of the labels of EARLIER batch
 // items adjacent to it; it pushes a 0-neighbour z unless an earlier batch item adjacent to z has
 // a non-WSHED label (serially that item pushed z first).  Both only wait on LOWER ranks.  Ranks
-// are dealt in chunks of RBS from an atomic dispenser in dispatch order (a block takes its next
-// chunk when it starts the current one), so every lower rank belongs to a chunk that a block
-// which is already running holds: the lowest unfinished chunk always has everything it waits on
-// finished, whatever the grid size and however many blocks are resident.  In-wave dependencies go through register shuffles, others through
+// are dealt round-robin over the grid (block-round r covers ranks [r*G*RBS, (r+1)*G*RBS)), so a
+// lower rank is in the same round or an earlier one.  Progress does not rest on the grid being
+// co-resident: a block claims each chunk as it starts it, and a wait that has lasted YIELD_TICKS
+// on a chunk nobody has claimed (its block is not resident, and the slots it needs may be held
+// by waiters) makes the waiting block give its chunk up and exit.  Everything a chunk writes
+// before it completes is idempotent (final and provisional granules, descriptors, cut words),
+// its histogram is added only on completion, and k_scan re-runs the batch (same epoch) until
+// every chunk has completed; a re-run skips completed chunks, so the lowest unfinished chunk
+// always completes.  In-wave dependencies go through register shuffles, others through
 // 8-byte granules {epoch, label} (final) or {epoch | bit 63, base fold} (provisional: a pending
 // dep whose settled neighbours fold to b can only end as b or WSHED).  Items then add their
 // pushes to the per-chunk level histograms and the cut words, which k_scan consumes.
@@ -836,7 +842,20 @@ __device__ Batch scan_body(const Ws& ws);
 __device__ void scatter_chunks(const Ws& ws, const Batch& B, int first, int stride);
 __device__ __forceinline__ void small_loop(const Ws& ws);
 
-__global__ __launch_bounds__(RBS, 6) void k_resolve(Ws ws) {
+// Cold path of k_resolve's long waits (out of line, so its registers stay off the hot loop): is
+// some chunk below `chunk` neither claimed in this run nor completed?
+__device__ __attribute__((noinline)) bool orphan_below(const unsigned long long* cflag, int chunk,
+                                                       unsigned long long ctag, unsigned epoch) {
+  bool orphan = false;
+  for (int c2 = lane_id(); c2 < chunk; c2 += 64)
+    if (__hip_atomic_load(&cflag[2 * c2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ctag &&
+        __hip_atomic_load(&cflag[2 * c2 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch)
+      orphan = true;
+  return orphan;
+}
+
+template <bool INJECT>
+__global__ __launch_bounds__(RBS, 4) void k_resolve(Ws ws) {
   Ctl* ctl = ws.ctl;
   const Batch B = ctl->bat;
   const bool work = !(B.n == 0 || B.mode != 0 || ctl->error);
@@ -849,19 +868,20 @@ __global__ __launch_bounds__(RBS, 6) void k_resolve(Ws ws) {
   const unsigned long long etag = (unsigned long long)B.epoch << 32;  // final label granule
   const unsigned long long ptag = etag | (1ull << 63);                // provisional base fold
   unsigned long long* const dg = ws.diag;
-  __shared__ int s_chunk, s_next;
-  if (tid == 0 && work) s_next = (int)atomicAdd(&ctl->rticket, 1u);
-  for (;;) {
-    if (!work) break;
-    if (tid == 0) {
-      s_chunk = s_next;
-      // the next chunk is claimed now, so its dispenser round trip overlaps this chunk's work
-      if ((long long)s_chunk * RBS < B.n) s_next = (int)atomicAdd(&ctl->rticket, 1u);
+  __shared__ int s_skip, s_yield;
+  __shared__ unsigned long long s_ctag;  // this run's chunk claims: {epoch, re-run}
+  if (tid == 0) s_ctag = etag | (unsigned)B.rrun;
+  if (tid == 0) s_yield = 0;
+  for (int base = blockIdx.x * RBS; work && base < B.n; base += gridDim.x * RBS) {
+    const int chunk = base / RBS;
+    if (tid == 0) {  // claim the chunk, or skip it when an earlier run of this batch completed it
+      s_skip = B.rrun > 0 &&
+               __hip_atomic_load(&ws.cflag[2 * chunk + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == B.epoch;
+      if (!s_skip) __hip_atomic_store(&ws.cflag[2 * chunk], s_ctag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tid < NQ) hist[tid] = 0;
     __syncthreads();
-    const int base = s_chunk * RBS;
-    if (base >= B.n) break;
+    if (s_skip) continue;
     const int wbase = base + (tid & ~63);
     const int i = wbase + lane;
     const bool valid = i < B.n;
@@ -879,6 +899,15 @@ __global__ __launch_bounds__(RBS, 6) void k_resolve(Ws ws) {
       it.wts = 0;
 #pragma unroll
       for (int k = 0; k < 16; ++k) it.dep[k] = -1;
+    }
+    if (INJECT && (blockIdx.x & 1) && base < (int)(gridDim.x * RBS) && B.rrun == 0) {
+      if (tid == 0) s_yield = 1;  // fault injection: exercise the give-up / re-run path
+      __syncthreads();
+      if (tid == 0) {
+        __hip_atomic_store(&ws.cflag[2 * chunk], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctl->rgive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      break;
     }
     unsigned inw = 0;  // wave-uniform: dependency slots that point inside this wave
     bool anydep = false;
@@ -1023,12 +1052,28 @@ __global__ __launch_bounds__(RBS, 6) void k_resolve(Ws ws) {
       if (!__any(!push_done)) break;
       if (++spins > 16) {
         __builtin_amdgcn_s_sleep(1);
-        if (__hip_atomic_load(&ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+        // {error, rgive}: stop on an error; give the chunk up when some block gave one up
+        const unsigned long long ew = __hip_atomic_load((unsigned long long*)&ctl->error, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+        if (ew) {
+          if (!(uint32_t)ew && lane == 0) s_yield = 1;
+          break;
+        }
         const long long now = (long long)__builtin_amdgcn_s_memrealtime();
         if (t0 == 0) t0 = now;
         else if (now - t0 > SPIN_LIMIT_TICKS) {
           if (!push_done) atomicOr(&ctl->error, ERR_TIMEOUT);
           break;
+        } else if ((spins & 255) == 0 && now - t0 > YIELD_TICKS) {
+          // a long wait: is every lower chunk claimed by a running block (or completed)?
+          const bool orphan = orphan_below(ws.cflag, chunk, *(volatile unsigned long long*)&s_ctag, B.epoch);
+          if (__any(orphan)) {
+            if (lane == 0) {
+              s_yield = 1;
+              __hip_atomic_store(&ctl->rgive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            break;
+          }
         }
       }
     }
@@ -1041,7 +1086,15 @@ __global__ __launch_bounds__(RBS, 6) void k_resolve(Ws ws) {
       atomicAdd(&dg[4], 1ull);
     }
     __syncthreads();
+    if (s_yield) {  // chunk given up: no histogram, no completion; k_scan re-runs the batch
+      if (tid == 0) {
+        __hip_atomic_store(&ws.cflag[2 * chunk], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctl->rgive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      break;
+    }
     if (tid < NQ && hist[tid]) atomicAdd(&ws.cnt[(long long)(base / CH) * NQ + tid], hist[tid]);
+    if (tid == 0) __hip_atomic_store(&ws.cflag[2 * chunk + 1], B.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (tid == 0 && s_minpush < NQ) atomicMin(&ctl->minpush, s_minpush);
@@ -1052,8 +1105,8 @@ __global__ __launch_bounds__(RBS, 6) void k_resolve(Ws ws) {
 // following small batches itself (small_loop).
 __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
   Ctl* ctl = ws.ctl;
-  if (threadIdx.x == 0) ctl->rticket = 0;  // this iteration's k_resolve has finished
   const Batch cb = scan_body(ws);
+  if (cb.mode == 2) return;  // k_resolve gave chunks up: the batch runs again, nothing committed
   if (cb.nchunk > 0 && cb.n <= SMALL_MAX && !ctl->error) {
     scatter_chunks(ws, cb, 0, 1);
     __syncthreads();
@@ -1102,7 +1155,18 @@ __device__ Batch scan_body(const Ws& ws) {
   }
   if (B.mode == 0 && tid < B.nseg) s_seg[tid] = ctl->seg[tid];
   const int cut = ctl->cut, segcut = ctl->segcut, minpush = ctl->minpush;
+  const int give = ctl->rgive;
   __syncthreads();
+  if (give && B.mode == 0) {  // a k_resolve block gave its chunk up: run the same batch again
+    if (tid == 0) {
+      ctl->rgive = 0;
+      ctl->cbat.n = 0;
+      ctl->cbat.nchunk = 0;
+      ctl->bat.rrun = B.rrun + 1;
+    }
+    none.mode = 2;
+    return none;
+  }
   int ncommit = B.n;
   if (B.mode == 0) {
     if (cut != NONE) ncommit = min(ncommit, cut + 1);
@@ -1160,6 +1224,7 @@ __device__ Batch scan_body(const Ws& ws) {
     nb.epoch = B.epoch + 1;
     nb.ncommit = 0;
     nb.nchunk = 0;
+    nb.rrun = 0;
     nb.nseg = ns;
     nb.n = (ns > 0) ? s_n : 0;
     nb.L = (ns > 0) ? nsegs[0].L : -1;
@@ -1512,6 +1577,7 @@ __device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qba
       nb.epoch = B.epoch + 1;
       nb.ncommit = 0;
       nb.nchunk = 0;
+      nb.rrun = 0;
       nb.nseg = *s_nseg;
       nb.n = (*s_nseg > 0) ? *s_n : 0;
       nb.L = (*s_nseg > 0) ? s_seg[0].L : -1;
@@ -1643,6 +1709,7 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
     nb.epoch = B0.epoch + 1;
     nb.ncommit = 0;
     nb.nchunk = 0;
+    nb.rrun = 0;
     nb.nseg = *s_nseg;
     nb.n = (*s_nseg > 0) ? *s_n : 0;
     nb.L = (*s_nseg > 0) ? s_seg[0].L : -1;
@@ -1852,6 +1919,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
       nb.epoch = B.epoch + 1;
       nb.ncommit = 0;
       nb.nchunk = 0;
+      nb.rrun = 0;
       nb.nseg = s_nseg;
       nb.n = (s_nseg > 0) ? s_n : 0;
       nb.L = (s_nseg > 0) ? s_seg[0].L : -1;

@@ -16,7 +16,7 @@ constexpr int INQ = -2;          // cv::watershed IN_QUEUE, before the pixel has
 __host__ __device__ inline int queued_state(int slot) { return -3 - slot; }
 __host__ __device__ inline int state_slot(int state) { return -3 - state; }
 constexpr int NONE = 0x7fffffff;
-constexpr int RBS = 512;           // threads per k_resolve block (3 co-resident per CU)
+constexpr int RBS = 512;           // threads per k_resolve block (2 per CU at its 128-VGPR budget)
 constexpr int SMALL_MAX = 4096;    // batches up to this size run in k_scan's one-workgroup loop
 constexpr int PAL_LDS_MAX = 16384; // palettes up to this many labels are staged in LDS
 constexpr int MERGE_CAP = 1 << 22; // largest multi-segment batch (items)
@@ -31,6 +31,7 @@ __host__ __device__ inline int next_wcap(int wcap, int n, int ncommit, bool icut
   return wcap;
 }
 constexpr long long SPIN_LIMIT_TICKS = 200000000ll;  // 2 s of s_memrealtime (100 MHz)
+constexpr long long YIELD_TICKS = 5000;              // 50 us: a k_resolve wait this long checks its owner
 
 // Per-pixel flood state is TILED: 4x4-pixel tiles of 8-byte {state, w4} words (128 B = one L2
 // line per tile), tiles row-major, Wt tiles per tile row.  A pixel and its 4 neighbours mostly
@@ -82,6 +83,7 @@ struct Batch {
   int ncommit;     // committed prefix (set by k_scan)
   int nchunk;      // chunks of the committed prefix (set by k_scan)
   int mode;        // 0 = flood batch, 1 = phase-1 pseudo-batch (items = ilist)
+  int rrun;        // k_resolve re-runs of this batch so far (chunks given up: see k_resolve)
 };
 
 struct Ctl {
@@ -96,14 +98,17 @@ struct Ctl {
   int minpush;  // lowest level pushed by the current batch (merge heuristic)
   int wcap;         // batch window (0 = whole buckets): shrinks after interrupt cuts, regrows
   int done;
-  int error;
+  int error;      // (8-aligned: k_resolve's waits load {error, rgive} as one word)
+  int rgive;      // a k_resolve block gave its chunk up this run (k_scan re-runs the batch)
   int remaining;  // queued items after the last batch was formed (host polling hint)
-  unsigned rticket;  // k_resolve's rank-chunk dispenser (dispatch order), reset by k_scan
   long long batches;
   long long pops;
   long long items;   // sum of batch sizes resolved (committed or not)
   long long pushes;  // committed pushes appended to buckets
 };
+
+static_assert(__builtin_offsetof(Ctl, error) % 8 == 0 && __builtin_offsetof(Ctl, rgive) == __builtin_offsetof(Ctl, error) + 4,
+              "Ctl.error and Ctl.rgive must share one aligned 8-byte word");
 
 struct Ws {
   const uint8_t* img;
@@ -119,6 +124,7 @@ struct Ws {
   int32_t* tot;      // phase-1 pixels per raster chunk (k_prep -> k_init_scan)
   int32_t* choff;
   unsigned* capp;    // CAP_SLOTS x NQ partial bucket-capacity histograms (k_prep -> k_init_scan)
+  unsigned long long* cflag;  // per k_resolve chunk: {epoch, run} of its claim, epoch of its completion
   Ctl* ctl;
   unsigned long long* diag;  // nullptr = off; else 8 counters (msg_set_diag)
   int* hmir;         // host-mapped progress mirror {iteration, done, error, remaining} (k_scatter)

@@ -120,7 +120,8 @@ class Segmenter:
         return out
 
     def set_diag(self, on=True):
-        self._check(self._L.msg_set_diag(self._h, 1 if on else 0))
+        """In-kernel counters; on=2 also injects k_resolve give-ups (tests of the re-run path)."""
+        self._check(self._L.msg_set_diag(self._h, 2 if on == 2 else (1 if on else 0)))
 
     # -- host buffers (numpy) -------------------------------------------------------------
     def watershed(self, bgr, markers):

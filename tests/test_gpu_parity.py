@@ -399,6 +399,20 @@ def test_resolve_grid_any_size(seg, blocks):
     assert hashlib.sha256(out.tobytes()).hexdigest() == dg["labels_sha256"]
 
 
+@pytest.mark.parametrize("kind,S", [("mosaic", 1024), ("mosaic_noise", 300), ("random", 256)])
+def test_resolve_give_up_and_rerun(seg, kind, S):
+    """Fault injection (msg_set_diag 2): k_resolve's odd blocks give up their first chunk of every
+    batch, so waiters on them give up too after their long-wait check, and k_scan re-runs the
+    batch until every chunk has completed.  Labels must still be the oracle's."""
+    img, m, d = synth.frame(kind, S, S, 5)
+    seg.set_diag(2)
+    try:
+        out = gpu_ws(seg, img, m)
+    finally:
+        seg.set_diag(False)
+    assert np.array_equal(out, ws_oracle.watershed(img, m))
+
+
 def test_two_contexts_two_threads():
     """Two Segmenters flooding at the same time from two host threads (the one-context-per-thread
     model of include/msegment.h), each with the full k_resolve grid: both bit-exact."""
