@@ -43,7 +43,7 @@ extern "C" {
 #define MSG_ERANGE   (-6)  /* output array too small / search space beyond what the
                               reference could finish (documented per entry point)          */
 
-#define MSG_ABI_VERSION 3
+#define MSG_ABI_VERSION 4
 
 typedef struct msg_ctx msg_ctx;
 
@@ -57,6 +57,12 @@ typedef struct msg_stats {
     int64_t diag[8];        /* msg_set_diag counters (0 when off): k_resolve gather cycles,
                                dependency-loop cycles, loop rounds, max loop cycles, wave-rounds;
                                small-batch loop rounds, small-batch loop entries; reserved      */
+    /* speculative generations (the interrupt-dense regime; msg_set_speculative) */
+    int64_t spec_generations;   /* generations committed                                        */
+    int64_t spec_rounds;        /* rounds run (every generation needs >= 2: run + confirm)      */
+    int64_t spec_executions;    /* item executions over all rounds                              */
+    int64_t spec_cascade_pops;  /* committed pops inside cascades (below the generation level)  */
+    int64_t spec_fallbacks;     /* overflowing executions handed to serial pops                 */
 } msg_stats;
 
 #define MSG_NKERNELS 20
@@ -84,6 +90,10 @@ int  msg_get_kernel_profile(msg_ctx* ctx, msg_kernel_profile* out, int max_entri
  * enable == 2 also injects faults for tests: the decision kernel's odd blocks give up their
  * first chunk of every batch once, which exercises the give-up / re-run path. */
 int  msg_set_diag(msg_ctx* ctx, int enable);
+/* Speculative generations for the interrupt-dense regime (textured frames, scattered seeds):
+ * on by default.  enable = 0 keeps the batch engine's serial pops there instead (A/B runs and
+ * tests of that path).  Results are identical either way (both are the exact serial order). */
+int  msg_set_speculative(msg_ctx* ctx, int enable);
 
 /* ---- host-buffer entry points (synchronous; strides in BYTES) ---------------------------- */
 

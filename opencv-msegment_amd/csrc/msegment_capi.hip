@@ -21,6 +21,7 @@
 
 #include "../../include/msegment.h"
 #include "ws_kernels.hip"
+#include "spec_kernels.hip"
 #include "nc_kernels.hip"
 #include "shape_kernels.hip"
 
@@ -44,6 +45,15 @@ struct msg_ctx {
   unsigned* d_capp = nullptr;  // CAP_SLOTS x NQ
   unsigned long long *d_tl = nullptr, *d_desc = nullptr, *d_cflag = nullptr;
   long long qcap = 0;
+  // speculative generations (spec_kernels.hip): allocated on the first flood that may use them
+  bool spec = true;             // msg_set_speculative
+  long long spec_np = 0, spec_logcap = 0;
+  unsigned long long *d_scl = nullptr, *d_sfin = nullptr, *d_stl = nullptr, *d_slog = nullptr;
+  unsigned long long *d_ssig = nullptr, *d_stmp = nullptr, *d_sflag = nullptr;
+  int32_t* d_slab = nullptr;
+  int2 *d_srec = nullptr, *d_sfrec = nullptr;
+  unsigned stag = 0;            // last round tag used (claims carry it; never reused)
+  int spec_grid = 0;            // k_spec_round blocks
   // staging for the host-buffer entry points
   long long stage_n = 0;
   uint8_t* d_img = nullptr;
@@ -95,14 +105,14 @@ struct msg_ctx {
 namespace {
 
 enum KernelId { KID_PREP, KID_INIT_SCAN, KID_COMPACT, KID_RESOLVE, KID_SCAN, KID_SCATTER,
-                KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_GRAY_HIST, KID_NC_MARKERS, KID_SPARE,
-                KID_GRAY, KID_MEDIAN, KID_CANNY, KID_CCL, KID_RING, KID_NUMBER, KID_HOLES, KID_SPARE2 };
+                KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_GRAY_HIST, KID_NC_MARKERS, KID_SPEC_ROUND,
+                KID_GRAY, KID_MEDIAN, KID_CANNY, KID_CCL, KID_RING, KID_NUMBER, KID_HOLES, KID_SPEC_FLATTEN };
 const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_compact", "k_resolve",
                                                 "k_scan", "k_scatter", "k_colorize",
                                                 "k_edge_weights", "k_untile", "k_gray_hist",
-                                                "k_nc_markers", "(unused)", "k_gray",
+                                                "k_nc_markers", "k_spec_round", "k_gray",
                                                 "k_median", "k_canny_nms", "k_ccl", "k_ring_median3",
-                                                "k_cc_number", "k_holes", "(unused)"};
+                                                "k_cc_number", "k_holes", "k_spec_flatten"};
 
 hipEvent_t pool_event(msg_ctx* c) {
   if (c->evused == c->evpool.size()) {
@@ -197,6 +207,44 @@ void free_flood(msg_ctx* c) {
   dfree(c->d_tl); dfree(c->d_desc); dfree(c->d_cflag);
   c->cap_n = c->cap_np = c->cap_rc = 0;
   c->qcap = 0;
+}
+
+void free_spec(msg_ctx* c) {
+  dfree(c->d_scl); dfree(c->d_sfin); dfree(c->d_stl); dfree(c->d_slog); dfree(c->d_ssig);
+  dfree(c->d_stmp); dfree(c->d_sflag); dfree(c->d_slab); dfree(c->d_srec); dfree(c->d_sfrec);
+  c->spec_np = c->spec_logcap = 0;
+  c->stag = 0;
+}
+
+// Speculative-generation workspace for np tiled pixels (n frame pixels): round claims and labels
+// (2 x 12 B), final claims (8 B) and the generation log (32 B) per pixel, per-rank arrays for
+// SPEC_WIN items, SPEC_RL records of scratch per k_spec_round thread.  Tags start at 1 on a
+// zeroed claim space and are never reused; near 2^31 the space is zeroed again.
+int ensure_spec(msg_ctx* c, long long np, long long n, hipStream_t st) {
+  const long long logcap = 4 * n + (1 << 20);
+  if (np <= c->spec_np && logcap <= c->spec_logcap && c->stag < 0x70000000u) return MSG_OK;
+  if (np > c->spec_np || logcap > c->spec_logcap) {
+    free_spec(c);
+    const long long slots = (long long)c->spec_grid * SPEC_BS;
+    HIPCHK(c, hipMalloc((void**)&c->d_scl, np * 2 * 8));
+    HIPCHK(c, hipMalloc((void**)&c->d_sfin, np * 8));
+    HIPCHK(c, hipMalloc((void**)&c->d_slab, np * 2 * 4));
+    HIPCHK(c, hipMalloc((void**)&c->d_stl, (size_t)SPEC_WIN * 8));
+    HIPCHK(c, hipMalloc((void**)&c->d_slog, logcap * 8));
+    HIPCHK(c, hipMalloc((void**)&c->d_srec, (size_t)2 * SPEC_WIN * sizeof(int2)));
+    HIPCHK(c, hipMalloc((void**)&c->d_ssig, (size_t)2 * SPEC_WIN * 8));
+    HIPCHK(c, hipMalloc((void**)&c->d_sfrec, (size_t)SPEC_WIN * sizeof(int2)));
+    HIPCHK(c, hipMalloc((void**)&c->d_stmp, slots * SPEC_RL * 8));
+    HIPCHK(c, hipMalloc((void**)&c->d_sflag, (size_t)(SPEC_WIN / SPEC_FT + 2) * 8));
+    c->spec_np = np;
+    c->spec_logcap = logcap;
+  }
+  HIPCHK(c, hipMemsetAsync(c->d_scl, 0, c->spec_np * 2 * 8, st));
+  HIPCHK(c, hipMemsetAsync(c->d_sfin, 0, c->spec_np * 8, st));
+  HIPCHK(c, hipMemsetAsync(c->d_stl, 0, (size_t)SPEC_WIN * 8, st));
+  HIPCHK(c, hipMemsetAsync(c->d_sflag, 0, (size_t)(SPEC_WIN / SPEC_FT + 2) * 8, st));
+  c->stag = 0;
+  return MSG_OK;
 }
 
 void free_stage(msg_ctx* c) {
@@ -321,6 +369,22 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   ws.N = N;
   ws.qcap = c->qcap;
 
+  // speculative generations: tiled indices must fit their 28-bit log field
+  const long long ntiled = (long long)((H + 3) / 4) * ws.Wt * 16;
+  const bool spec = c->spec && ntiled <= (1ll << 28) && H >= 3 && W >= 3;
+  ws.scl = nullptr; ws.sfin = nullptr; ws.slab = nullptr; ws.stl = nullptr; ws.slog = nullptr;
+  ws.srec = nullptr; ws.ssig = nullptr; ws.sfrec = nullptr; ws.stmp = nullptr; ws.sflag = nullptr;
+  ws.snp = 0;
+  ws.slogcap = 0;
+  if (spec) {
+    rc = ensure_spec(c, ntiled, N, st);
+    if (rc) return rc;
+    ws.scl = c->d_scl; ws.sfin = c->d_sfin; ws.slab = c->d_slab; ws.stl = c->d_stl;
+    ws.slog = c->d_slog; ws.srec = c->d_srec; ws.ssig = c->d_ssig; ws.sfrec = c->d_sfrec;
+    ws.stmp = c->d_stmp; ws.sflag = c->d_sflag;
+    ws.snp = c->spec_np;
+    ws.slogcap = c->spec_logcap;
+  }
   const int npx = (int)((N + CH - 1) / CH);
   const int gres = std::max(1, std::min(c->res_grid, (int)((N + RBS - 1) / RBS)));
   const int gsc = std::min(npx * (CH / 1024), 1024);
@@ -330,7 +394,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)npx * NQ * sizeof(int32_t), st));
   const int nrc = H * ws.nseg;  // raster chunks
   LAUNCH(c, KID_PREP, st, k_prep, dim3((H + 3) / 4 * ws.nseg), dim3(RSEG), 0, ws, d_mk_in);
-  LAUNCH(c, KID_INIT_SCAN, st, k_init_scan, dim3(1), dim3(1024), 0, ws, nrc, c->epoch);
+  LAUNCH(c, KID_INIT_SCAN, st, k_init_scan, dim3(1), dim3(1024), 0, ws, nrc, c->epoch, c->stag);
   LAUNCH(c, KID_COMPACT, st, k_compact, dim3((nrc + 4 * CPW - 1) / (4 * CPW)), dim3(256), 0, ws, nrc);
   LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
   LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, -1);
@@ -340,15 +404,28 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   // host-mapped mirror that each iteration's k_scatter writes (no copy kernel, no event wait):
   // after queueing a group the host spins until the previous group's last iteration reported.
   __atomic_store_n(&c->h_mir[0], -1, __ATOMIC_RELEASE);
+  c->h_mir[4] = 0;
   int it = 0, prev_end = -1;
   c->group = 4;
   long long syncs = 0;
+  // Two kinds of iteration, chosen per group from the regime the last poll reported (a stale
+  // choice only costs no-op launches: every kernel checks the batch mode it serves, and k_scan
+  // commits only decided batches): batches (k_resolve) or a speculative generation's rounds and
+  // flattening (k_spec_round x SPEC_ITER_ROUNDS, k_spec_flatten), then the common commit.
+  constexpr int SPEC_ITER_ROUNDS = 3;
+  const int gflat = std::max(1, c->cus);
   for (;;) {
+    const bool spec_it = spec && c->h_mir[4] != 0;
     for (int g = 0; g < c->group; ++g, ++it) {
-      if (c->inject)  // test only: odd blocks give up their first chunk (msg_set_diag 2)
+      if (spec_it) {
+        for (int r = 0; r < SPEC_ITER_ROUNDS; ++r)
+          LAUNCH(c, KID_SPEC_ROUND, st, k_spec_round, dim3(c->spec_grid), dim3(SPEC_BS), 0, ws);
+        LAUNCH(c, KID_SPEC_FLATTEN, st, k_spec_flatten, dim3(gflat), dim3(SPEC_FT), 0, ws);
+      } else if (c->inject) {  // test only: odd blocks give up their first chunk (msg_set_diag 2)
         LAUNCH(c, KID_RESOLVE, st, k_resolve<true>, dim3(gres), dim3(RBS), 0, ws);
-      else
+      } else {
         LAUNCH(c, KID_RESOLVE, st, k_resolve<false>, dim3(gres), dim3(RBS), 0, ws);
+      }
       LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);  // + small batches
       LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, it);
     }
@@ -386,6 +463,12 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   c->stats.pushes = tail.pushes;
   for (int k = 0; k < 8; ++k) c->stats.diag[k] = (int64_t)dgv[k];
   c->stats.host_syncs = syncs;
+  c->stats.spec_generations = tail.spec.gens;
+  c->stats.spec_rounds = tail.spec.rounds_total;
+  c->stats.spec_executions = tail.spec.execs;
+  c->stats.spec_cascade_pops = tail.spec.cpops;
+  c->stats.spec_fallbacks = tail.spec.fallbacks;
+  if (spec) c->stag = tail.spec.T;
   c->epoch += (unsigned)std::min<long long>(tail.batches + 4, 0x7fffffff);
   if (tail.error & ERR_TIMEOUT)
     return fail(c, MSG_ETIMEOUT, "in-kernel wait timed out (grid not co-resident?)");
@@ -460,7 +543,10 @@ int run_batch(msg_ctx* c, int n, F fn) {
   // up to min(k, hardware queues) floods run kernels concurrently (streams beyond the HIP
   // runtime's hardware queues share them and serialise).  k_resolve deals its rank chunks in
   // dispatch order, so concurrent grids need not be co-resident: each keeps the full grid.
-  for (int w = 0; w < k; ++w) c->subs[w]->res_grid = c->res_grid;
+  for (int w = 0; w < k; ++w) {
+    c->subs[w]->res_grid = c->res_grid;
+    c->subs[w]->spec = c->spec;
+  }
   std::vector<int> rcs(k, MSG_OK);
   std::vector<msg_stats> st(k);
   std::vector<std::thread> th;
@@ -609,7 +695,7 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
   c->dev = device_ordinal;
   if (hipSetDevice(c->dev) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void**)&c->d_ctl, sizeof(Ctl)) != hipSuccess ||
-      hipHostMalloc((void**)&c->h_mir, 4 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) !=
+      hipHostMalloc((void**)&c->h_mir, 8 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer((void**)&c->d_mir, c->h_mir, 0) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
@@ -630,6 +716,7 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
     // depend on how many of the blocks are resident (msg_set_resolve_grid overrides it)
     c->res_grid = cus * std::max(1, std::min(per, 4));
     c->cus = cus;
+    c->spec_grid = 2 * cus;  // 64 KB of cascade queues per block: two blocks per CU
   }
   *out = c;
   return MSG_OK;
@@ -640,6 +727,7 @@ void msg_destroy(msg_ctx* c) {
   (void)hipSetDevice(c->dev);
   if (c->own) (void)hipStreamSynchronize(c->own);
   free_flood(c);
+  free_spec(c);
   for (msg_ctx* sub : c->subs) msg_destroy(sub);
   c->subs.clear();
   free_stage(c);
@@ -668,6 +756,13 @@ const char* msg_last_error(const msg_ctx* c) { return c ? c->err.c_str() : "null
 int msg_get_stats(const msg_ctx* c, msg_stats* out) {
   if (!c || !out) return MSG_EINVAL;
   *out = c->stats;
+  return MSG_OK;
+}
+
+int msg_set_speculative(msg_ctx* c, int enable) {
+  if (!c) return MSG_EINVAL;
+  c->spec = enable != 0;
+  for (msg_ctx* sub : c->subs) sub->spec = c->spec;
   return MSG_OK;
 }
 

@@ -1,0 +1,571 @@
+// spec_kernels.hip -- speculative generations: the exact flood's interrupt-dense regime (gfx950).
+//
+// cv::watershed (OpenCV 3.4.2, reached from PictureService.java:909) pops the
+// oldest item of the lowest non-empty bucket.  On textured frames almost every few pops push a
+// neighbour below the popped level (an "interrupt"), and the batch engine of ws_kernels.hip, which
+// cuts a batch right after such an item, degenerates to a few pops per batch.  Here a GENERATION
+// is the whole lowest bucket L instead (ranks 0..n-1 in FIFO order), never cut at interrupts:
+//
+//   * item j's EXECUTION is what the serial run does from its pop until the next item of bucket L
+//     pops: the pop of its pixel (label = fold of labelled neighbours, pushes of unknown ones in
+//     L,R,T,B order) followed by its CASCADE -- every push below L, popped lowest level first,
+//     FIFO within a level, to exhaustion (a cascade only ever pops pixels it pushed itself);
+//     pushes at levels >= L are deferred to the buckets in execution order;
+//   * executions are speculative and repeated in ROUNDS.  Item j reads what items < j wrote:
+//     the top pops of earlier adjacent items of the CURRENT round (waited for, as k_resolve
+//     does: ranks are dealt in dispatch order, so every wait is on a running wave), everything
+//     else through the PREVIOUS round's claims.  The serial order is the unique fixed point of
+//     this triangular system, reached when no execution changes between two rounds; the stable
+//     prefix P (items unchanged since the previous round, all of whose inputs are therefore
+//     final) grows every round and is never executed again;
+//   * CLAIMS: per pixel and round parity one 64-bit word {round tag, rank, popped} written with
+//     atomicMax on the inverted rank (the lowest rank wins, newer rounds win), the popper's label
+//     in a parallel array; an item recognises its own writes by its own rank.  Final items'
+//     claims are promoted to one word {generation tag, popped, label} per pixel;
+//   * commit (k_spec_flatten): the final executions of items 0..P-1 in rank order ARE the serial
+//     pop sequence of the generation.  Flattened into "virtual items" (one per pop, with its
+//     deferred pushes) they go through the batch engine's own ordered append (k_scan,
+//     k_scatter), which keeps every bucket in exact serial FIFO order;
+//   * an execution that overflows its lane's queue (SPEC_QCAP live entries) or scratch
+//     (SPEC_RL records) while all its inputs are final ends the regime: the prefix before it is
+//     committed and the batch engine pops that item and its cascade (serial pops), after which
+//     the regime resumes (SpecCtl.block).
+// scripts/exp/spec_rounds.c is the CPU prototype of exactly this scheme (bit-exact against the
+// oracle on mosaic+noise, random and album frames; it also counts the rounds).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ws_shared.h"
+
+namespace msg {
+
+constexpr unsigned SPEC_RMAX = (1u << 22) - 1;
+
+__device__ __forceinline__ unsigned long long spec_claim(unsigned tag, int rank, unsigned popped) {
+  return ((unsigned long long)tag << 32) | ((unsigned long long)(SPEC_RMAX - (unsigned)rank) << 1) | popped;
+}
+__device__ __forceinline__ unsigned sc_tag(unsigned long long c) { return (unsigned)(c >> 32); }
+__device__ __forceinline__ int sc_rank(unsigned long long c) {
+  return (int)(SPEC_RMAX - (unsigned)((c >> 1) & SPEC_RMAX));
+}
+// Words written inside a round are read with agent-scope atomics (L2, never a stale L1 line).
+__device__ __forceinline__ unsigned long long ld_ag64(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_ag32(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_ag64(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_ag32(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void claim_max(unsigned long long* p, unsigned long long k) {
+  __hip_atomic_fetch_max(p, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long fin_word(unsigned G, unsigned popped, int lab) {
+  return ((unsigned long long)G << 33) | ((unsigned long long)popped << 32) | (uint32_t)lab;
+}
+// generation log record: label | deferred-push mask | tiled pixel (< 2^28)
+__device__ __forceinline__ unsigned long long srec_pack(int p, int lab, unsigned dm) {
+  return ((unsigned long long)(uint32_t)lab << 32) | ((unsigned long long)dm << 28) | (unsigned)p;
+}
+__device__ __forceinline__ unsigned long long smix(unsigned long long h, unsigned long long v) {
+  h ^= v + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+  return h * 0xff51afd7ed558ccdull;
+}
+
+struct SpecView {
+  const unsigned long long* cur;   // this round's claims
+  const unsigned long long* prev;  // the previous round's (valid when hasprev)
+  const unsigned long long* fin;
+  const int32_t* slc;
+  const int32_t* slp;
+  unsigned T, G;
+  bool hasprev;
+};
+
+// State of pixel z as item j sees it: > 0 label, WSHED, 0 unknown, INQ queued or pushed.
+// Own writes first, then final items' writes, then the previous round's lower ranks, else the
+// pre-generation state.
+__device__ __forceinline__ int spec_view(const Ws& ws, const SpecView& V, int j, int z, bool own) {
+  const unsigned long long o = own ? ld_ag64(V.cur + z) : 0ull;
+  const unsigned long long f = ld_ag64(V.fin + z);
+  const unsigned long long c = V.hasprev ? V.prev[z] : 0ull;
+  const int s = ws.mk[z];
+  if (own && sc_tag(o) == V.T && sc_rank(o) == j) return (o & 1ull) ? ld_ag32(V.slc + z) : INQ;
+  if ((unsigned)(f >> 33) == V.G) return ((f >> 32) & 1ull) ? (int)(uint32_t)f : INQ;
+  if (V.hasprev && sc_tag(c) == V.T - 1 && sc_rank(c) < j) return (c & 1ull) ? V.slp[z] : INQ;
+  return (s >= WSHED) ? s : INQ;
+}
+
+// top-pop granule of item k as item j may use it in round T: this round's, or a final item's
+__device__ __forceinline__ bool spec_granule(const Ws& ws, int k, int P, unsigned T, unsigned G, int& v) {
+  const unsigned long long g = ld_ag64(ws.stl + k);
+  const unsigned tg = (unsigned)(g >> 32);
+  if (tg == T || (k < P && tg >= G && tg <= T)) {
+    v = (int)(uint32_t)g;
+    return true;
+  }
+  return false;
+}
+
+// End of a round (last block): grow the stable prefix, or hand the generation to the commit.
+__device__ void spec_finalize(Ctl* ctl, int P, int n, unsigned T, unsigned G) {
+  SpecCtl& s = ctl->spec;
+  // written by this kernel's atomics: read at L2, not through a line cached at kernel start
+  const int fc = __hip_atomic_load(&s.fc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int ov = __hip_atomic_load(&s.ovfr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int newP = min(fc, n);
+  s.rounds_total += 1;
+  if (newP >= n) {
+    s.Pprom = P;
+    s.P = n;
+    s.state = 2;
+  } else if ((newP == P && T > G && ov == newP) || (s.rounds >= SPEC_ROUNDS_MAX && newP == 0)) {
+    // item newP read only final inputs and still overflowed: commit the prefix, pop it serially
+    s.Pprom = P;
+    s.P = newP;
+    s.state = 2;
+    s.fallback = 1;
+  } else if (s.rounds >= SPEC_ROUNDS_MAX) {
+    s.Pprom = P;
+    s.P = newP;
+    s.state = 2;
+  } else {
+    s.Pold = P;
+    s.P = newP;
+    s.T = T + 1;
+    s.rounds += 1;
+    s.deal = P;
+    s.fc = NONE;
+    s.ovfr = NONE;
+  }
+  s.ticket = 0;
+}
+
+// One round.  Waves take 64 consecutive ranks at a time from [Pold, n) in dispatch order:
+// [Pold, P) promote their claims, [P, n) execute.
+__global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
+  Ctl* ctl = ws.ctl;
+  if (ctl->bat.mode != 3 || ctl->spec.state != 1 || ctl->error) return;
+  __shared__ unsigned long long lq[SPEC_QCAP * SPEC_BS];  // per-lane cascade queues, [entry][lane]
+  __shared__ int s_exec;
+  const int tid = threadIdx.x, lane = lane_id();
+  if (tid == 0) s_exec = 0;
+  const unsigned T = ctl->spec.T, G = ctl->spec.G;
+  const int P = ctl->spec.P, n = ctl->spec.n, L = ctl->spec.L, bstart = ctl->spec.bstart;
+  const long long np = ws.snp;
+  const int par = (int)(T & 1u), ppar = (int)((T - 1u) & 1u);
+  SpecView V;
+  V.cur = ws.scl + (size_t)par * np;
+  V.prev = ws.scl + (size_t)ppar * np;
+  V.fin = ws.sfin;
+  V.slc = ws.slab + (size_t)par * np;
+  V.slp = ws.slab + (size_t)ppar * np;
+  V.T = T;
+  V.G = G;
+  V.hasprev = T > G;
+  unsigned long long* const cur = ws.scl + (size_t)par * np;
+  int32_t* const slc = ws.slab + (size_t)par * np;
+  unsigned long long* const tmp = ws.stmp + (size_t)(blockIdx.x * SPEC_BS + tid) * SPEC_RL;
+  const unsigned long long etag = (unsigned long long)T << 32;
+  const int Wt = ws.Wt, marg = ws.marg;
+  bool stop = false;
+  __syncthreads();
+  while (!stop) {
+    int r0 = 0;
+    if (lane == 0) r0 = atomicAdd(&ctl->spec.deal, 64);
+    r0 = __shfl(r0, 0);
+    if (r0 >= n) break;
+    const int j = r0 + lane;
+    // ---- promote: final since the last round; their claims become permanent ----
+    if (j < P) {
+      const int2 rc = ws.srec[(size_t)ppar * SPEC_WIN + j];
+      ws.sfrec[j] = rc;
+      for (int k = 0; k < rc.y; ++k) {
+        const unsigned long long r = ws.slog[rc.x + k];
+        const int y = (int)(r & 0x0fffffffu);
+        const unsigned dm = (unsigned)(r >> 28) & 15u;
+        st_ag64(ws.sfin + y, fin_word(G, 1u, (int)(uint32_t)(r >> 32)));
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          if ((dm >> d) & 1u) st_ag64(ws.sfin + (nbi(y + marg, d, Wt) - marg), fin_word(G, 0u, 0));
+      }
+    }
+    // ---- execute [P, n): gather the top pop ----
+    const bool ex = j >= P && j < n;
+    int p = 0;
+    unsigned wp = 0, zm = 0;
+    int nbp[4] = {0, 0, 0, 0}, dep[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dep[k] = -1;
+    int base_lab = 0;
+    if (ex) {
+      p = ws.qbuf[bstart + j];
+      wp = (unsigned)ws.w4[p];
+      const int pb = p + marg;
+      int s4[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        nbp[d] = nbi(pb, d, Wt) - marg;
+        s4[d] = ws.mk[nbp[d]];
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        if (s4[d] <= -3) {  // an earlier item of this generation: its top pop of this round
+          const int k = state_slot(s4[d]) - bstart;
+          if (k >= 0 && k < j) {
+            dep[d] = k;
+            continue;
+          }
+        }
+        const int v = spec_view(ws, V, j, nbp[d], false);
+        if (v > 0) base_lab = fold_lab(base_lab, v);
+        else if (v == 0) zm |= 1u << d;
+      }
+      if (base_lab != WSHED) {  // competitors for the unknown neighbours: earlier adjacent items
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          if (!((zm >> d) & 1u)) continue;
+          const int zb = nbp[d] + marg;
+          const int ee[3] = {(d == 1) ? 1 : 0, (d <= 1) ? 2 : 1, (d == 2) ? 2 : 3};
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const int sz = ws.mk[nbi(zb, ee[k], Wt) - marg];
+            if (sz <= -3) {
+              const int r = state_slot(sz) - bstart;
+              if (r >= 0 && r < j) dep[4 + 3 * d + k] = r;
+            }
+          }
+        }
+      }
+    }
+    // ---- wait for the earlier adjacent top pops of this round (lower ranks only) ----
+    bool labd = !ex, pushd = !ex;
+    int mylab = 0;
+    unsigned pm = 0;
+    bool ovf = false;
+    long long t0 = 0;
+    int spins = 0;
+    for (;;) {
+      if (!labd) {
+        int lab = base_lab;
+        bool unk = false;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          if (dep[d] < 0) continue;
+          int v;
+          if (spec_granule(ws, dep[d], P, T, G, v)) {
+            if (v > 0) lab = fold_lab(lab, v);
+          } else {
+            unk = true;
+          }
+        }
+        if (lab == WSHED || !unk) {
+          if (lab == 0) {  // cannot happen for a queued pixel; unstable, never committed
+            ovf = true;
+            lab = WSHED;
+          }
+          mylab = lab;
+          labd = true;
+          st_ag64(ws.stl + j, etag | (uint32_t)lab);
+        }
+      }
+      if (labd && !pushd) {
+        if (mylab == WSHED) {
+          pushd = true;
+        } else {
+          bool und = false;
+          unsigned m = 0;
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            if (!((zm >> d) & 1u)) continue;
+            bool lose = false, u = false;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              const int r = dep[4 + 3 * d + k];
+              if (r < 0) continue;
+              int v;
+              if (spec_granule(ws, r, P, T, G, v)) {
+                if (v > 0) lose = true;  // that item pushed the neighbour first
+              } else {
+                u = true;
+              }
+            }
+            if (!lose) {
+              if (u) und = true;
+              else m |= 1u << d;
+            }
+          }
+          if (!und) {
+            pm = m;
+            pushd = true;
+          }
+        }
+      }
+      if (!__any(!pushd)) break;
+      if (++spins > 16) {
+        __builtin_amdgcn_s_sleep(1);
+        if (ld_ag32(&ctl->error)) {
+          stop = true;
+          break;
+        }
+        const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+        if (t0 == 0) {
+          t0 = now;
+        } else if (now - t0 > SPIN_LIMIT_TICKS) {
+          if (!pushd) atomicOr(&ctl->error, ERR_TIMEOUT);
+          stop = true;
+          break;
+        }
+      }
+    }
+    if (stop) break;
+    if (!ex) continue;
+    // ---- the top pop's writes, then the cascade (levels < L, lowest first, FIFO) ----
+    claim_max(cur + p, spec_claim(T, j, 1u));
+    st_ag32(slc + p, mylab);
+    int nq = 0;
+    unsigned dm = 0;
+    if (mylab != WSHED) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        if (!((pm >> d) & 1u)) continue;
+        const int z = nbp[d];
+        claim_max(cur + z, spec_claim(T, j, 0u));
+        const unsigned t = (wp >> (8 * d)) & 255u;
+        if ((int)t < L) {
+          if (nq < SPEC_QCAP) lq[(nq++) * SPEC_BS + tid] = ((unsigned long long)t << 32) | (unsigned)z;
+          else ovf = true;
+        } else {
+          dm |= 1u << d;
+        }
+      }
+    }
+    unsigned long long rec = srec_pack(p, mylab, dm);
+    unsigned long long sig = smix(0x6a09e667f3bcc908ull, rec);
+    tmp[0] = rec;
+    int nrec = 1;
+    while (nq > 0 && !ovf) {
+      int bi = 0;
+      unsigned long long be = lq[tid];
+      for (int k = 1; k < nq; ++k) {
+        const unsigned long long e = lq[k * SPEC_BS + tid];
+        if ((e >> 32) < (be >> 32)) {
+          be = e;
+          bi = k;
+        }
+      }
+      for (int k = bi; k + 1 < nq; ++k) lq[k * SPEC_BS + tid] = lq[(k + 1) * SPEC_BS + tid];
+      --nq;
+      if (nrec >= SPEC_RL) {
+        ovf = true;
+        break;
+      }
+      const int y = (int)(uint32_t)be;
+      const unsigned wy = (unsigned)ws.w4[y];
+      const int yb = y + marg;
+      int nby[4], v[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) nby[d] = nbi(yb, d, Wt) - marg;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) v[d] = spec_view(ws, V, j, nby[d], true);
+      int lab = 0;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        if (v[d] > 0) lab = fold_lab(lab, v[d]);
+      if (lab == 0) {  // own writes hidden by a conflicting lower rank: unstable
+        ovf = true;
+        lab = WSHED;
+      }
+      claim_max(cur + y, spec_claim(T, j, 1u));
+      st_ag32(slc + y, lab);
+      unsigned dmy = 0;
+      if (lab != WSHED) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          if (v[d] != 0) continue;
+          const int z = nby[d];
+          claim_max(cur + z, spec_claim(T, j, 0u));
+          const unsigned t = (wy >> (8 * d)) & 255u;
+          if ((int)t < L) {
+            if (nq < SPEC_QCAP) lq[(nq++) * SPEC_BS + tid] = ((unsigned long long)t << 32) | (unsigned)z;
+            else ovf = true;
+          } else {
+            dmy |= 1u << d;
+          }
+        }
+      }
+      rec = srec_pack(y, lab, dmy);
+      tmp[nrec++] = rec;
+      sig = smix(sig, rec);
+    }
+    int base = 0;
+    if (!ovf) {
+      base = atomicAdd(&ctl->spec.logtop, nrec);
+      if ((long long)base + nrec > ws.slogcap) ovf = true;  // generation log full: unstable
+      else
+        for (int k = 0; k < nrec; ++k) ws.slog[base + k] = tmp[k];
+    }
+    sig = smix(sig, ((unsigned long long)nrec << 1) | (ovf ? 1ull : 0ull));
+    ws.srec[(size_t)par * SPEC_WIN + j] = make_int2(base, ovf ? 0 : nrec);
+    ws.ssig[(size_t)par * SPEC_WIN + j] = sig;
+    const bool changed = !V.hasprev || ovf || ws.ssig[(size_t)ppar * SPEC_WIN + j] != sig;
+    if (changed) atomicMin(&ctl->spec.fc, j);
+    if (ovf) atomicMin(&ctl->spec.ovfr, j);
+    atomicAdd(&s_exec, 1);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    atomicAdd((unsigned long long*)&ctl->spec.execs, (unsigned long long)s_exec);
+    __threadfence();
+    if (atomicAdd(&ctl->spec.ticket, 1) == (int)gridDim.x - 1) {
+      __threadfence();
+      spec_finalize(ctl, P, n, T, G);
+    }
+  }
+}
+
+// The generation's commit as an ordinary batch of "virtual items" (one per pop, in serial
+// order) for k_scan / k_scatter: pixel, label and deferred-push descriptor per virtual rank, the
+// per-chunk level histograms, and the batch header: n = pops, one segment advancing bucket L's
+// head by P.  Tiles of SPEC_FT items are dealt in dispatch order and chained (a tile waits only
+// for the tile before it, held by a running block).
+__global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
+  Ctl* ctl = ws.ctl;
+  if (ctl->bat.mode != 3 || ctl->spec.state != 2 || ctl->error) return;
+  SpecCtl& s = ctl->spec;
+  const int P = s.P, Pprom = s.Pprom, L = s.L, bstart = s.bstart;
+  const unsigned T = s.T, G = s.G;
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const unsigned long long etag = (unsigned long long)ctl->bat.epoch << 32;
+  __shared__ int s_tile, s_off, s_tot;
+  __shared__ int wsum[SPEC_FT / 64];
+  if (P == 0) {  // nothing final (overflow at rank 0): the batch engine takes the bucket's head
+    if (blockIdx.x == 0 && tid == 0) {
+      Batch nb = ctl->bat;
+      nb.mode = 0;
+      nb.n = min(s.n, WMIN);
+      nb.nseg = 1;
+      nb.ncommit = 0;
+      nb.nchunk = 0;
+      nb.rrun = 0;
+      Seg sg;
+      sg.L = L;
+      sg.bstart = bstart;
+      sg.rank = 0;
+      sg.n = nb.n;
+      ctl->seg[0] = sg;
+      ctl->cut = NONE;
+      ctl->segcut = NONE;
+      ctl->minpush = 0;
+      ctl->wcap = WMIN;
+      s.on = 0;
+      s.block = L;
+      s.fallbacks += 1;
+      s.state = 0;
+      ctl->bat = nb;  // undecided (rsv != epoch): k_scan leaves it to the small-batch loop
+    }
+    return;
+  }
+  const int ntiles = (P + SPEC_FT - 1) / SPEC_FT;
+  for (;;) {
+    if (tid == 0) s_tile = atomicAdd(&s.ftile, 1);
+    __syncthreads();
+    const int tile = s_tile;
+    if (tile >= ntiles) break;
+    const int j = tile * SPEC_FT + tid;
+    int2 rc = make_int2(0, 0);
+    if (j < P) rc = (j < Pprom) ? ws.sfrec[j] : ws.srec[(size_t)(T & 1u) * SPEC_WIN + j];
+    int x = rc.y;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    int excl = x - rc.y, tot = 0;
+#pragma unroll
+    for (int k = 0; k < SPEC_FT / 64; ++k) {
+      if (k < wv) excl += wsum[k];
+      tot += wsum[k];
+    }
+    if (tid == 0) {
+      int prev = 0;
+      if (tile > 0) {
+        long long t0 = 0;
+        for (;;) {
+          const unsigned long long f = ld_ag64(ws.sflag + tile - 1);
+          if ((unsigned)(f >> 32) == G) {
+            prev = (int)(uint32_t)f;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+          if (t0 == 0) t0 = now;
+          else if (now - t0 > SPIN_LIMIT_TICKS) {
+            atomicOr(&ctl->error, ERR_TIMEOUT);
+            break;
+          }
+        }
+      }
+      st_ag64(ws.sflag + tile, ((unsigned long long)G << 32) | (uint32_t)(prev + tot));
+      s_off = prev;
+      s_tot = prev + tot;
+    }
+    __syncthreads();
+    const int v0 = s_off + excl;
+    for (int k = 0; k < rc.y; ++k) {
+      const unsigned long long r = ws.slog[rc.x + k];
+      const int y = (int)(r & 0x0fffffffu);
+      const unsigned dm = (unsigned)(r >> 28) & 15u;
+      const int v = v0 + k;
+      const unsigned wy = (unsigned)ws.w4[y];
+      ws.ipx[v] = y;
+      ws.tl[v] = etag | (uint32_t)(r >> 32);
+      ws.desc[v] = make_desc(wy, dm, L, 0);
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        if ((dm >> d) & 1u) atomicAdd(&ws.cnt[(long long)(v / CH) * NQ + ((wy >> (8 * d)) & 255u)], 1);
+    }
+    if (tile == ntiles - 1 && tid == 0) {  // the batch header (read by the next kernel)
+      const int Vn = s_tot;
+      Batch nb = ctl->bat;
+      nb.mode = 0;
+      nb.n = Vn;
+      nb.nseg = 1;
+      nb.ncommit = 0;
+      nb.nchunk = 0;
+      nb.rrun = 0;
+      Seg sg;
+      sg.L = L;
+      sg.bstart = bstart;
+      sg.rank = 0;
+      sg.n = P;  // k_scan advances bucket L's head by min(pops, P) = P
+      ctl->seg[0] = sg;
+      ctl->cut = NONE;
+      ctl->segcut = NONE;
+      ctl->minpush = 0;  // no multi-segment merge right after a generation
+      ctl->rsv = nb.epoch;
+      s.gens += 1;
+      s.cpops += Vn - P;
+      if (s.fallback) {
+        s.on = 0;
+        s.block = L;
+        s.fallbacks += 1;
+        ctl->wcap = WMIN;
+      } else if (Vn == P && s.n >= SPEC_QUIET) {  // a large generation without a cascade: batches pay
+        s.on = 0;
+        s.block = 0;
+      }
+      s.state = 0;
+      ctl->bat = nb;
+    }
+    __syncthreads();  // s_tile / wsum reused
+  }
+}
+
+}  // namespace msg

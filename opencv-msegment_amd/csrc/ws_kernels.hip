@@ -508,10 +508,42 @@ __device__ __forceinline__ void load_segs(const Ctl* ctl, const Batch& B, Seg* s
   for (int k = threadIdx.x; k < B.nseg; k += blockDim.x) s[k] = ctl->seg[k];
 }
 
+// Turn the next batch into a speculative generation (k_spec_round): the whole lowest bucket L
+// (navail items from bstart, at most SPEC_WIN), round tags continuing from the last round.
+// One thread; nb.epoch is already set.
+__device__ void spec_begin(Ctl* ctl, Batch& nb, int L, int bstart, int navail) {
+  SpecCtl& s = ctl->spec;
+  nb.mode = 3;
+  nb.nseg = 1;
+  nb.L = L;
+  nb.bstart = bstart;
+  nb.n = min(navail, SPEC_WIN);
+  nb.ncommit = 0;
+  nb.nchunk = 0;
+  nb.rrun = 0;
+  s.G = s.T + 1;
+  s.T = s.G;
+  s.L = L;
+  s.n = nb.n;
+  s.bstart = bstart;
+  s.P = 0;
+  s.Pold = 0;
+  s.Pprom = 0;
+  s.rounds = 1;
+  s.state = 1;
+  s.fc = NONE;
+  s.ovfr = NONE;
+  s.deal = 0;
+  s.ticket = 0;
+  s.logtop = 0;
+  s.fallback = 0;
+  s.ftile = 0;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Init scan (1 block x 1024): bucket bases from the capacity histogram; exclusive scan of the
 // per-chunk phase-1 counts (compaction offsets); sets up the phase-1 pseudo-batch.
-__global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigned epoch0) {
+__global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigned epoch0, unsigned stag0) {
   Ctl* ctl = ws.ctl;
   const int tid = threadIdx.x;
   __shared__ long long wsum[16];
@@ -618,6 +650,7 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
     ctl->cut = NONE;
     ctl->segcut = NONE;
     ctl->minpush = 0;  // the first flood batch is never merged
+    ctl->spec.T = stag0;  // speculative round tags continue from the context's last one
     if (M == 0) ctl->done = 1;
   }
 }
@@ -871,6 +904,7 @@ __global__ __launch_bounds__(RBS, 4) void k_resolve(Ws ws) {
   __shared__ int s_skip, s_yield;
   __shared__ unsigned long long s_ctag;  // this run's chunk claims: {epoch, re-run}
   if (tid == 0) s_ctag = etag | (unsigned)B.rrun;
+  if (work && blockIdx.x == 0 && tid == 0) ctl->rsv = B.epoch;  // k_scan commits only decided batches
   if (tid == 0) s_yield = 0;
   for (int base = blockIdx.x * RBS; work && base < B.n; base += gridDim.x * RBS) {
     const int chunk = base / RBS;
@@ -1140,6 +1174,16 @@ __device__ Batch scan_body(const Ws& ws) {
     }
     return none;
   }
+  if (B.mode == 3 || (B.mode == 0 && ctl->rsv != B.epoch)) {
+    // not decided yet: speculative rounds still running, or an iteration without k_resolve
+    // (the host queued the other iteration kind): nothing to commit here
+    __syncthreads();
+    if (tid == 0) {
+      ctl->cbat.n = 0;
+      ctl->cbat.nchunk = 0;
+    }
+    return none;
+  }
   // the queue state lives in LDS for the whole kernel: one parallel load, one write-back
   __shared__ int partial[NQ];
   __shared__ int s_head[NQ], s_tail[NQ], s_base[NQ];
@@ -1229,6 +1273,8 @@ __device__ Batch scan_body(const Ws& ws) {
     nb.n = (ns > 0) ? s_n : 0;
     nb.L = (ns > 0) ? nsegs[0].L : -1;
     nb.bstart = (ns > 0) ? nsegs[0].bstart : 0;
+    if (ns > 0 && ctl->spec.on)
+      spec_begin(ctl, nb, nsegs[0].L, nsegs[0].bstart, s_tail[nsegs[0].L] - s_head[nsegs[0].L]);
     ctl->bat = nb;
     ctl->wcap = wcap;
     ctl->cut = NONE;
@@ -1371,6 +1417,7 @@ __global__ __launch_bounds__(1024) void k_scatter(Ws ws, int iter) {
     __hip_atomic_store(ws.hmir + 1, ws.ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 2, ws.ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 3, ws.ctl->remaining, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 4, ws.ctl->spec.on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const Batch B = ws.ctl->cbat;
@@ -1626,7 +1673,8 @@ __device__ __forceinline__ int lowest_bucket(const int* head, const int* tail, i
 }
 
 __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qbase, int* s_head, int* s_tail,
-                            int* s_wcap, int* s_err, int* s_nseg, int* s_n, int* s_ser, long long* cnt) {
+                            int* s_wcap, int* s_err, int* s_nseg, int* s_n, int* s_ser, long long* cnt,
+                            int spec_block) {
   const int lane = lane_id();
   const int Wt = ws.Wt, marg = ws.marg;
   const Batch B0 = *s_B;
@@ -1641,6 +1689,7 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
       continue;
     }
     if (run >= SERIAL_RUN) break;
+    if (spec_block > 0 && lo >= spec_block) break;  // the cascade that stopped the speculative engine is done
     if (lo != ring_l || h >= ring_h0 + ring_n) {  // the bucket's next 64 slots, one load per lane
       ring_l = lo;
       ring_h0 = h;
@@ -1731,6 +1780,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
   __shared__ Seg s_seg[NQ];
   __shared__ int s_cut, s_segcut, s_minpush, s_err, s_nseg, s_n, s_wcap;
   __shared__ int s_ser;  // 1: the interrupt-dense regime, tiny batches popped serially
+  __shared__ int s_specgo, s_specblk;  // hand the regime to the speculative engine; its resume level
   __shared__ Batch s_B;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const int Wt = ws.Wt;
@@ -1739,6 +1789,8 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     s_err = ctl->error;
     s_wcap = ctl->wcap;
     s_ser = 0;
+    s_specgo = 0;
+    s_specblk = ws.scl ? ctl->spec.block : -1;  // -1: engine off
   }
   if (tid < NQ) {
     s_qbase[tid] = ctl->qbase[tid];
@@ -1758,9 +1810,15 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     if (B.n <= TINY_MAX) {  // runs of tiny batches: wave 0 alone, the other waves wait here
       if (wv == 0) {
         long long c4[4] = {0, 0, 0, 0};
-        if (s_ser)
-          serial_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, c4);
-        else
+        if (s_ser && s_specblk >= 0 && lowest_bucket(s_head, s_tail, 0) >= s_specblk) {
+          if (lane == 0) s_specgo = 1;  // interrupt-dense: speculative generations from here on
+        } else if (s_ser) {
+          serial_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, c4,
+                      s_specblk > 0 ? s_specblk : 0);
+          // the cascade that stopped the speculative engine is done: hand the regime back to it
+          // (not to a whole-bucket batch that the next interrupt cuts again)
+          if (s_specblk > 0 && s_B.n > 0 && lowest_bucket(s_head, s_tail, 0) >= s_specblk && lane == 0) s_specgo = 1;
+        } else
           tiny_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, s_wcnt[0], &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, c4);
         if (tid == 0) {
           nb_pops += c4[0];
@@ -1770,6 +1828,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
         }
       }
       __syncthreads();
+      if (s_specgo) break;
       continue;
     }
     for (int k = tid; k < B.n; k += 1024) s_lab[k] = 0;
@@ -1945,7 +2004,13 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
   if (tid == 0) ctl->remaining = q;
   for (int k = tid; k < s_B.nseg; k += 1024) ctl->seg[k] = s_seg[k];
   if (tid == 0) {
-    ctl->bat = s_B;
+    Batch nb = s_B;
+    if (s_specgo) {
+      spec_begin(ctl, nb, nb.L, s_qbase[nb.L] + s_head[nb.L], s_tail[nb.L] - s_head[nb.L]);
+      ctl->spec.on = 1;
+      ctl->spec.block = 0;
+    }
+    ctl->bat = nb;
     ctl->wcap = s_wcap;
     ctl->cut = NONE;
     ctl->segcut = NONE;

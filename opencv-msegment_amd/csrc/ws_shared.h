@@ -59,6 +59,40 @@ constexpr int ERR_TIMEOUT = 1;
 constexpr int ERR_STATE = 2;
 constexpr int ERR_CAPACITY = 4;
 
+// Speculative generations (k_spec_round / k_spec_flatten, ws_kernels.hip): the interrupt-dense
+// regime.  A generation is the whole lowest bucket; each item's execution is its own pop plus its
+// cascade (every level below the bucket's, to exhaustion), repeated in rounds until no execution
+// changes (the serial result is the unique fixed point: item i depends only on items < i).
+constexpr int SPEC_WIN = 1 << 20;   // items per generation (claim ranks have 22 bits)
+constexpr int SPEC_BS = 256;        // threads per k_spec_round block
+constexpr int SPEC_QCAP = 32;       // per-lane cascade queue (LDS): more live entries = overflow
+constexpr int SPEC_RL = 256;        // records per execution (lane scratch): more = overflow
+constexpr int SPEC_ROUNDS_MAX = 64; // rounds per generation before the stable prefix is committed
+constexpr int SPEC_FT = 1024;       // items per k_spec_flatten tile
+constexpr int SPEC_QUIET = 4096;    // a generation this large without a cascade ends the regime
+
+struct SpecCtl {
+  unsigned T;     // current round tag: round claims in scl[T & 1], labels in slab[T & 1]
+  unsigned G;     // tag of the generation's first round (final claims carry it)
+  int L, n, bstart;
+  int P;          // stable prefix: items < P are final
+  int Pold;       // items [Pold, P) are final but not yet promoted (their claims -> sfin)
+  int Pprom;      // at flatten: items < Pprom were promoted (records via sfrec)
+  int rounds;     // rounds of this generation so far
+  int state;      // 0 none, 1 rounds running, 2 ready to flatten
+  int on;         // regime: batches are speculative generations
+  int block;      // after a fallback: the regime may resume once the lowest level is >= block
+  int fc;         // lowest rank whose execution changed this round (atomicMin)
+  int ovfr;       // lowest rank that overflowed this round (atomicMin)
+  int deal;       // dispatch-order rank dealing
+  int ticket;     // blocks finished this round
+  int logtop;     // generation log records used
+  int fallback;   // the commit ends the regime (overflow at the stable prefix)
+  int ftile;      // k_spec_flatten tile dealing
+  int pad;
+  long long gens, rounds_total, execs, cpops, fallbacks;
+};
+
 // desc word of a batch item: bits 0-31 the 4 edge weights, 32-35 push (or 0-neighbour) mask,
 // 40-47 the item's level, 48-55 its segment.
 __host__ __device__ inline unsigned long long make_desc(unsigned wts, unsigned mask, int lv, int sg) {
@@ -105,6 +139,9 @@ struct Ctl {
   long long pops;
   long long items;   // sum of batch sizes resolved (committed or not)
   long long pushes;  // committed pushes appended to buckets
+  unsigned rsv;      // epoch of the last batch k_resolve (or k_spec_flatten) decided
+  int pad;
+  SpecCtl spec;
 };
 
 static_assert(__builtin_offsetof(Ctl, error) % 8 == 0 && __builtin_offsetof(Ctl, rgive) == __builtin_offsetof(Ctl, error) + 4,
@@ -127,7 +164,21 @@ struct Ws {
   unsigned long long* cflag;  // per k_resolve chunk: {epoch, run} of its claim, epoch of its completion
   Ctl* ctl;
   unsigned long long* diag;  // nullptr = off; else 8 counters (msg_set_diag)
-  int* hmir;         // host-mapped progress mirror {iteration, done, error, remaining} (k_scatter)
+  int* hmir;         // host-mapped progress mirror {iteration, done, error, remaining, spec} (k_scatter)
+  // speculative generations (nullptr when the engine is off); claims and labels are indexed by
+  // tiled pixel like mk, one array of snp entries per round parity
+  unsigned long long* scl;   // 2 x snp round claims {tag, rank, popped}
+  unsigned long long* sfin;  // snp final claims {generation tag, popped, label}
+  int32_t* slab;             // 2 x snp labels of popped pixels
+  unsigned long long* stl;   // SPEC_WIN top-pop granules {round tag, label}
+  unsigned long long* slog;  // generation log: records {label, dmask, pixel}
+  int2* srec;                // 2 x SPEC_WIN {log base, records} per round parity
+  unsigned long long* ssig;  // 2 x SPEC_WIN execution signatures
+  int2* sfrec;               // SPEC_WIN {log base, records} of promoted items
+  unsigned long long* stmp;  // lane scratch: SPEC_RL records per k_spec_round thread
+  unsigned long long* sflag; // k_spec_flatten tile prefixes {generation tag, inclusive sum}
+  long long snp;
+  long long slogcap;
   int H, W;
   int Wt;            // tiles per tile row = ceil(W / 4)
   int marg;          // tiled entries of margin before mk / w4 (mk - marg starts the state array)

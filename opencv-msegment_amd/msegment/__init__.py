@@ -123,6 +123,10 @@ class Segmenter:
         """In-kernel counters; on=2 also injects k_resolve give-ups (tests of the re-run path)."""
         self._check(self._L.msg_set_diag(self._h, 2 if on == 2 else (1 if on else 0)))
 
+    def set_speculative(self, on=True):
+        """Speculative generations for the interrupt-dense regime (default on); off = serial pops."""
+        self._check(self._L.msg_set_speculative(self._h, 1 if on else 0))
+
     # -- host buffers (numpy) -------------------------------------------------------------
     def watershed(self, bgr, markers):
         """cv::watershed(bgr, markers): ``markers`` (int32 (H, W) ndarray) is rewritten in place."""

@@ -29,7 +29,7 @@ EXPORTS = (
     "msg_create", "msg_destroy", "msg_last_error", "msg_abi_version", "msg_get_stats",
     "msg_watershed", "msg_colorize", "msg_watershed_colorize", "msg_watershed_batch",
     "msg_watershed_dev", "msg_colorize_dev", "msg_watershed_colorize_dev", "msg_edge_weights_dev",
-    "msg_set_profiling", "msg_get_kernel_profile", "msg_set_diag",
+    "msg_set_profiling", "msg_get_kernel_profile", "msg_set_diag", "msg_set_speculative",
     "msg_set_batch_inflight", "msg_set_resolve_grid", "msg_watershed_colorize_batch_dev",
     "msg_gray_hist_dev", "msg_nc_levels", "msg_nc_marker_lut", "msg_nc_markers_dev",
     "msg_nc_marker_stage_dev", "msg_nc_marker_stage",
@@ -49,7 +49,10 @@ class Stats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_int64), ("pops", ctypes.c_int64),
                 ("host_syncs", ctypes.c_int64), ("rows", ctypes.c_int64), ("cols", ctypes.c_int64),
                 ("items", ctypes.c_int64), ("pushes", ctypes.c_int64),
-                ("diag", ctypes.c_int64 * 8)]
+                ("diag", ctypes.c_int64 * 8),
+                ("spec_generations", ctypes.c_int64), ("spec_rounds", ctypes.c_int64),
+                ("spec_executions", ctypes.c_int64), ("spec_cascade_pops", ctypes.c_int64),
+                ("spec_fallbacks", ctypes.c_int64)]
 
 
 class KernelProfile(ctypes.Structure):
@@ -121,6 +124,8 @@ def load():
     L.msg_set_profiling.restype = i
     L.msg_set_diag.argtypes = [vp, i]
     L.msg_set_diag.restype = i
+    L.msg_set_speculative.argtypes = [vp, i]
+    L.msg_set_speculative.restype = i
     L.msg_get_kernel_profile.argtypes = [vp, ctypes.POINTER(KernelProfile), i, i]
     L.msg_get_kernel_profile.restype = i
     L.msg_set_batch_inflight.argtypes = [vp, i]

@@ -26,7 +26,7 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_binding_load():
     L = _lib.load()
-    assert L.msg_abi_version() == 3
+    assert L.msg_abi_version() == 4
 
 
 def test_library_is_gfx950_code_object():
