@@ -294,7 +294,9 @@ def stress_line(seg, S, sync, dev, steps, cpu=True, kind="mosaic_noise", seed=2)
                        "(BASELINE config 3 stress variant)" % (kind, S, S, seed),
            "value": round(S * S * steps / dt / 1e6, 3), "unit": "Mpx/s", "steps": steps,
            "ms_per_step": round(1000.0 * dt / steps, 3), "parity": parity,
-           "flood": {"batches": st["batches"], "pops": st["pops"], "items": st["items"]}}
+           "flood": {"batches": st["batches"], "pops": st["pops"], "items": st["items"],
+                     "spec_generations": st["spec_generations"], "spec_rounds": st["spec_rounds"],
+                     "spec_executions": st["spec_executions"], "spec_fallbacks": st["spec_fallbacks"]}}
     if cpu:
         c, cl = cpu_baseline(img, m, depth, budget_s=8.0, max_reps=5)
         out["cpu_baseline"] = c
@@ -401,7 +403,7 @@ def main(argv=None):
                          "shape: shapeAutoMarkerWatershed's (median, Canny, rings, components)")
     ap.add_argument("--nc-depth", type=int, default=4, help="user depth of the nc pipeline")
     ap.add_argument("--nc-options", default="GISTO_DIAP", help="comma list: GISTO_DIAP,MULTI_OTSU")
-    ap.add_argument("--stress-steps", type=int, default=2,
+    ap.add_argument("--stress-steps", type=int, default=5,
                     help="steps of the config-3 stress line (mosaic+noise at --size); 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile-pass", action="store_true")

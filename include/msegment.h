@@ -56,7 +56,11 @@ typedef struct msg_stats {
     int64_t pushes;         /* queue appends after phase 1                                    */
     int64_t diag[8];        /* msg_set_diag counters (0 when off): k_resolve gather cycles,
                                dependency-loop cycles, loop rounds, max loop cycles, wave-rounds;
-                               small-batch loop rounds, small-batch loop entries; reserved      */
+                               small-batch loop rounds, small-batch loop entries; reserved.
+                               When speculative generations ran: wave time in top-pop waits,
+                               in cascades, in the round kernel (10 ns ticks), longest wave,
+                               most records of an execution, longest wait, longest cascade,
+                               waves                                                            */
     /* speculative generations (the interrupt-dense regime; msg_set_speculative) */
     int64_t spec_generations;   /* generations committed                                        */
     int64_t spec_rounds;        /* rounds run (every generation needs >= 2: run + confirm)      */
@@ -171,6 +175,11 @@ int msg_edge_weights_dev(msg_ctx* ctx, const void* d_bgr, void* d_wright, void* 
                                    level's mean instead of the mean alone (:799-808)        */
 #define MSG_NC_MULTI_OTSU 0x2u  /* AlgorithmOptions.MULTI_OTSU: replace the levels by the
                                    multi-Otsu split of the 128-bin histogram (:650-722)     */
+#define MSG_NC_MEDIAN_BLUR 0x4u /* AlgorithmOptions.MEDIAN_BLUR: medianBlur(srcGray, k) before
+                                   the histogram (:481-483); k = filterMaskSize in option
+                                   bits 8-15 (MSG_NC_MASK(k)), odd, else MSG_EINVAL.  The
+                                   BILATERIAL branch (:487-494) is not provided.             */
+#define MSG_NC_MASK(k) (((unsigned)(k) & 0xffu) << 8)
 
 typedef struct msg_bright_level {  /* model/BrightLevel.java */
     int32_t start, end, count;
@@ -202,8 +211,8 @@ int msg_nc_marker_lut(const msg_bright_level* levels, int n_levels, unsigned opt
 int msg_nc_markers_dev(msg_ctx* ctx, const void* d_gray, int rows, int cols,
                        const int32_t* lut256, void* d_markers, void* stream);
 
-/* The whole marker stage: gray + histogram -> levels -> markers.  d_gray may be NULL (context
- * scratch).  The level count is the watershed depth the reference then uses (:834): draw the
+/* The whole marker stage: gray (MSG_NC_MEDIAN_BLUR: then its k x k median) + histogram ->
+ * levels -> markers.  d_gray (the final srcGray) may be NULL (context scratch).  The level count is the watershed depth the reference then uses (:834): draw the
  * palettes for it and call msg_watershed_colorize_dev(d_bgr, d_markers, ...). */
 int msg_nc_marker_stage_dev(msg_ctx* ctx, const void* d_bgr, int rows, int cols, int depth,
                             unsigned options, void* d_gray, void* d_markers,

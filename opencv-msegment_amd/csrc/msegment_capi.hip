@@ -51,7 +51,8 @@ struct msg_ctx {
   unsigned long long *d_scl = nullptr, *d_sfin = nullptr, *d_stl = nullptr, *d_slog = nullptr;
   unsigned long long *d_ssig = nullptr, *d_stmp = nullptr, *d_sflag = nullptr;
   int32_t* d_slab = nullptr;
-  int2 *d_srec = nullptr, *d_sfrec = nullptr;
+  int4* d_srec = nullptr;
+  int2* d_sfrec = nullptr;
   unsigned stag = 0;            // last round tag used (claims carry it; never reused)
   int spec_grid = 0;            // k_spec_round blocks
   // staging for the host-buffer entry points
@@ -92,6 +93,8 @@ struct msg_ctx {
   unsigned* h_hist = nullptr;
   uint8_t* d_gscr = nullptr;
   long long gscr_n = 0;
+  uint8_t* d_gscr2 = nullptr;  // unblurred gray of the NC MEDIAN_BLUR branch
+  long long gscr2_n = 0;
   // shape marker stage: 6 byte planes, 2 int planes (parents, block keys), 2 block-key arrays,
   // scan scratch, 4 counters
   long long sh_n = 0, sh_nb = 0;
@@ -231,7 +234,7 @@ int ensure_spec(msg_ctx* c, long long np, long long n, hipStream_t st) {
     HIPCHK(c, hipMalloc((void**)&c->d_slab, np * 2 * 4));
     HIPCHK(c, hipMalloc((void**)&c->d_stl, (size_t)SPEC_WIN * 8));
     HIPCHK(c, hipMalloc((void**)&c->d_slog, logcap * 8));
-    HIPCHK(c, hipMalloc((void**)&c->d_srec, (size_t)2 * SPEC_WIN * sizeof(int2)));
+    HIPCHK(c, hipMalloc((void**)&c->d_srec, (size_t)2 * SPEC_WIN * sizeof(int4)));
     HIPCHK(c, hipMalloc((void**)&c->d_ssig, (size_t)2 * SPEC_WIN * 8));
     HIPCHK(c, hipMalloc((void**)&c->d_sfrec, (size_t)SPEC_WIN * sizeof(int2)));
     HIPCHK(c, hipMalloc((void**)&c->d_stmp, slots * SPEC_RL * 8));
@@ -390,7 +393,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   const int gsc = std::min(npx * (CH / 1024), 1024);
   HIPCHK(c, hipMemsetAsync(c->d_ctl, 0, sizeof(Ctl), st));
   HIPCHK(c, hipMemsetAsync(c->d_capp, 0, (size_t)CAP_SLOTS * NQ * 4, st));
-  if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 8 * sizeof(unsigned long long), st));
+  if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 16 * sizeof(unsigned long long), st));
   HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)npx * NQ * sizeof(int32_t), st));
   const int nrc = H * ws.nseg;  // raster chunks
   LAUNCH(c, KID_PREP, st, k_prep, dim3((H + 3) / 4 * ws.nseg), dim3(RSEG), 0, ws, d_mk_in);
@@ -452,7 +455,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   }
   Ctl tail;
   HIPCHK(c, hipMemcpyAsync(&tail, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
-  unsigned long long dgv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long dgv[16] = {0};
   if (c->diag) HIPCHK(c, hipMemcpyAsync(dgv, c->d_diag, sizeof(dgv), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
   ++syncs;
@@ -461,7 +464,8 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   c->stats.pops = tail.pops;
   c->stats.items = tail.items;
   c->stats.pushes = tail.pushes;
-  for (int k = 0; k < 8; ++k) c->stats.diag[k] = (int64_t)dgv[k];
+  // when speculative generations ran, diag reports their round split instead (spec_kernels.hip)
+  for (int k = 0; k < 8; ++k) c->stats.diag[k] = (int64_t)dgv[tail.spec.gens ? 8 + k : k];
   c->stats.host_syncs = syncs;
   c->stats.spec_generations = tail.spec.gens;
   c->stats.spec_rounds = tail.spec.rounds_total;
@@ -595,8 +599,9 @@ int stream_grid(long long N) {
 
 bool aligned(const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
 
+// from_gray: d_bgr is a gray plane to histogram (no gray output)
 int gray_hist(msg_ctx* c, const uint8_t* d_bgr, long long N, uint8_t* d_gray, int32_t* hist,
-              hipStream_t st) {
+              hipStream_t st, bool from_gray = false) {
   if (!c->d_hist) {
     HIPCHK(c, hipMalloc((void**)&c->d_hist, 256 * sizeof(unsigned)));
     HIPCHK(c, hipHostMalloc((void**)&c->h_hist, 256 * sizeof(unsigned), hipHostMallocDefault));
@@ -609,7 +614,10 @@ int gray_hist(msg_ctx* c, const uint8_t* d_bgr, long long N, uint8_t* d_gray, in
   // one block per CU (fewer when the frame is small)
   const long long per_block = (long long)GH_BS * GH_UNROLL;
   const int grid = (int)std::max<long long>(1, std::min<long long>(c->cus, ((N >> 2) + per_block - 1) / per_block));
-  LAUNCH(c, KID_GRAY_HIST, st, k_gray_hist, dim3(grid), dim3(GH_BS), 0, d_bgr, N, d_gray, c->d_hist);
+  if (from_gray)
+    LAUNCH(c, KID_GRAY_HIST, st, k_gray_hist<true>, dim3(grid), dim3(GH_BS), 0, d_bgr, N, d_gray, c->d_hist);
+  else
+    LAUNCH(c, KID_GRAY_HIST, st, k_gray_hist<false>, dim3(grid), dim3(GH_BS), 0, d_bgr, N, d_gray, c->d_hist);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->h_hist, c->d_hist, 256 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
@@ -716,7 +724,7 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
     // depend on how many of the blocks are resident (msg_set_resolve_grid overrides it)
     c->res_grid = cus * std::max(1, std::min(per, 4));
     c->cus = cus;
-    c->spec_grid = 2 * cus;  // 64 KB of cascade queues per block: two blocks per CU
+    c->spec_grid = 2 * cus;  // k_spec_round: 64 KB of LDS cascade queues per block, two per CU
   }
   *out = c;
   return MSG_OK;
@@ -736,6 +744,7 @@ void msg_destroy(msg_ctx* c) {
   dfree(c->d_diag);
   dfree(c->d_hist);
   dfree(c->d_gscr);
+  dfree(c->d_gscr2);
   dfree(c->d_sh8);
   dfree(c->d_sh32);
   dfree(c->d_shF);
@@ -776,7 +785,7 @@ int msg_set_diag(msg_ctx* c, int enable) {
   if (!c) return MSG_EINVAL;
   if (enable && !c->d_diag) {
     HIPCHK(c, hipSetDevice(c->dev));
-    HIPCHK(c, hipMalloc((void**)&c->d_diag, 8 * sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc((void**)&c->d_diag, 16 * sizeof(unsigned long long)));
   }
   c->diag = enable != 0;
   c->inject = enable == 2;
@@ -1096,7 +1105,31 @@ int msg_nc_marker_stage_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, i
     g = c->d_gscr;
   }
   int32_t hist[256];
-  rc = gray_hist(c, (const uint8_t*)d_bgr, N, g, hist, st);
+  if (options & MSG_NC_MEDIAN_BLUR) {
+    // medianBlur(srcGray, srcGray, filterMaskSize) (:481-483), then the histogram of the result
+    const int k = (int)((options >> 8) & 0xffu);
+    if (k < 1 || (k & 1) == 0)
+      return fail(c, MSG_EINVAL, "MEDIAN_BLUR mask size %d: must be odd (medianBlur's assertion)", k);
+    if (N > 0) {
+      if (c->gscr2_n < N) {
+        dfree(c->d_gscr2);
+        c->gscr2_n = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_gscr2, N + 16));
+        c->gscr2_n = N;
+      }
+      const int grid = (int)std::max<long long>(1, std::min<long long>(8192, (N + 255) / 256));
+      LAUNCH(c, KID_GRAY, st, k_gray, dim3(grid), dim3(256), 0, (const uint8_t*)d_bgr, N, c->d_gscr2);
+      if (k > 1)
+        LAUNCH(c, KID_MEDIAN, st, k_median, dim3((cols + MED_BS - 1) / MED_BS, (rows + MED_ROWS - 1) / MED_ROWS),
+               dim3(MED_BS), 0, c->d_gscr2, g, rows, cols, k);
+      else
+        HIPCHK(c, hipMemcpyAsync(g, c->d_gscr2, N, hipMemcpyDeviceToDevice, st));
+      HIPCHK(c, hipGetLastError());
+    }
+    rc = gray_hist(c, g, N, nullptr, hist, st, true);
+  } else {
+    rc = gray_hist(c, (const uint8_t*)d_bgr, N, g, hist, st);
+  }
   if (rc) return rc;
   int n = 0;
   std::vector<msg_bright_level> all(256);  // at most one level closes per bin 1..255

@@ -33,6 +33,9 @@ __device__ __forceinline__ uint32_t gray_of(uint32_t b, uint32_t g, uint32_t r) 
 // 256 sums to hist with global atomics: with one block per CU that is 256 atomics per bin.
 // (scripts/exp/hist_variants.hip: one sub-histogram per wave costs 3x on a flat frame; 4096
 // blocks of global atomics, or a last-block reduction over per-block partials, cost 4x.)
+// FROM_GRAY: `bgr` is already a gray plane (the MEDIAN_BLUR branch, :481-483, histograms the
+// blurred srcGray): one dword of 4 pixels per group, no gray output.
+template <bool FROM_GRAY>
 __global__ __launch_bounds__(GH_BS) void k_gray_hist(const uint8_t* __restrict__ bgr, long long N,
                                                      uint8_t* __restrict__ gray,
                                                      unsigned* __restrict__ hist) {
@@ -51,22 +54,35 @@ __global__ __launch_bounds__(GH_BS) void k_gray_hist(const uint8_t* __restrict__
     for (int u = 0; u < GH_UNROLL; ++u) {
       const long long q = q0 + (long long)u * GH_BS;
       if (q < nq) {
-        w[u][0] = b32[3 * q];
-        w[u][1] = b32[3 * q + 1];
-        w[u][2] = b32[3 * q + 2];
+        if (FROM_GRAY) {
+          w[u][0] = b32[q];
+        } else {
+          w[u][0] = b32[3 * q];
+          w[u][1] = b32[3 * q + 1];
+          w[u][2] = b32[3 * q + 2];
+        }
       }
     }
 #pragma unroll
     for (int u = 0; u < GH_UNROLL; ++u) {
       const long long q = q0 + (long long)u * GH_BS;
       if (q >= nq) break;
-      // B0 G0 R0 B1 | G1 R1 B2 G2 | R2 B3 G3 R3
-      const uint32_t w0 = w[u][0], w1 = w[u][1], w2 = w[u][2];
-      const uint32_t y0 = gray_of(w0 & 255u, (w0 >> 8) & 255u, (w0 >> 16) & 255u);
-      const uint32_t y1 = gray_of(w0 >> 24, w1 & 255u, (w1 >> 8) & 255u);
-      const uint32_t y2 = gray_of((w1 >> 16) & 255u, w1 >> 24, w2 & 255u);
-      const uint32_t y3 = gray_of((w2 >> 8) & 255u, (w2 >> 16) & 255u, w2 >> 24);
-      reinterpret_cast<uint32_t*>(gray)[q] = y0 | (y1 << 8) | (y2 << 16) | (y3 << 24);
+      uint32_t y0, y1, y2, y3;
+      if (FROM_GRAY) {
+        const uint32_t g4 = w[u][0];
+        y0 = g4 & 255u;
+        y1 = (g4 >> 8) & 255u;
+        y2 = (g4 >> 16) & 255u;
+        y3 = g4 >> 24;
+      } else {
+        // B0 G0 R0 B1 | G1 R1 B2 G2 | R2 B3 G3 R3
+        const uint32_t w0 = w[u][0], w1 = w[u][1], w2 = w[u][2];
+        y0 = gray_of(w0 & 255u, (w0 >> 8) & 255u, (w0 >> 16) & 255u);
+        y1 = gray_of(w0 >> 24, w1 & 255u, (w1 >> 8) & 255u);
+        y2 = gray_of((w1 >> 16) & 255u, w1 >> 24, w2 & 255u);
+        y3 = gray_of((w2 >> 8) & 255u, (w2 >> 16) & 255u, w2 >> 24);
+        reinterpret_cast<uint32_t*>(gray)[q] = y0 | (y1 << 8) | (y2 << 16) | (y3 << 24);
+      }
       const uint32_t yw = __builtin_amdgcn_readfirstlane(y0);
       const unsigned nact = (unsigned)__popcll(__ballot(1));
       if (__all(y0 == yw && y1 == yw && y2 == yw && y3 == yw)) {
@@ -81,8 +97,13 @@ __global__ __launch_bounds__(GH_BS) void k_gray_hist(const uint8_t* __restrict__
   }
   if (blockIdx.x == 0 && tid < (int)(N & 3)) {  // ragged tail (< 4 pixels)
     const long long p = (nq << 2) + tid;
-    const uint32_t y = gray_of(bgr[3 * p], bgr[3 * p + 1], bgr[3 * p + 2]);
-    gray[p] = (uint8_t)y;
+    uint32_t y;
+    if (FROM_GRAY) {
+      y = bgr[p];
+    } else {
+      y = gray_of(bgr[3 * p], bgr[3 * p + 1], bgr[3 * p + 2]);
+      gray[p] = (uint8_t)y;
+    }
     atomicAdd(mine + y, 1u);
   }
   __syncthreads();

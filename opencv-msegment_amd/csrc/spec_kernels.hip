@@ -90,13 +90,16 @@ struct SpecView {
 // Own writes first, then final items' writes, then the previous round's lower ranks, else the
 // pre-generation state.
 __device__ __forceinline__ int spec_view(const Ws& ws, const SpecView& V, int j, int z, bool own) {
+  // every word loaded up front (labels too, used or not): one memory round trip per view
   const unsigned long long o = own ? ld_ag64(V.cur + z) : 0ull;
-  const unsigned long long f = ld_ag64(V.fin + z);
+  const int lc = own ? ld_ag32(V.slc + z) : 0;
+  const unsigned long long f = V.fin[z];  // promotes racing this load: prev covers them
   const unsigned long long c = V.hasprev ? V.prev[z] : 0ull;
+  const int lp = V.hasprev ? V.slp[z] : 0;
   const int s = ws.mk[z];
-  if (own && sc_tag(o) == V.T && sc_rank(o) == j) return (o & 1ull) ? ld_ag32(V.slc + z) : INQ;
+  if (own && sc_tag(o) == V.T && sc_rank(o) == j) return (o & 1ull) ? lc : INQ;
   if ((unsigned)(f >> 33) == V.G) return ((f >> 32) & 1ull) ? (int)(uint32_t)f : INQ;
-  if (V.hasprev && sc_tag(c) == V.T - 1 && sc_rank(c) < j) return (c & 1ull) ? V.slp[z] : INQ;
+  if (V.hasprev && sc_tag(c) == V.T - 1 && sc_rank(c) < j) return (c & 1ull) ? lp : INQ;
   return (s >= WSHED) ? s : INQ;
 }
 
@@ -112,8 +115,12 @@ __device__ __forceinline__ bool spec_granule(const Ws& ws, int k, int P, unsigne
 }
 
 // End of a round (last block): grow the stable prefix, or hand the generation to the commit.
-__device__ void spec_finalize(Ctl* ctl, int P, int n, unsigned T, unsigned G) {
+__device__ void spec_finalize(Ctl* ctl, int P, int n, unsigned T, unsigned G, unsigned long long* dg) {
   SpecCtl& s = ctl->spec;
+  if (dg) {  // diagnostics: sum over rounds of the round's longest wave
+    dg[5] += __hip_atomic_load(&s.rmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s.rmax = 0;
+  }
   // written by this kernel's atomics: read at L2, not through a line cached at kernel start
   const int fc = __hip_atomic_load(&s.fc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int ov = __hip_atomic_load(&s.ovfr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -173,6 +180,10 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
   const unsigned long long etag = (unsigned long long)T << 32;
   const int Wt = ws.Wt, marg = ws.marg;
   bool stop = false;
+  unsigned long long* const dg = ws.diag ? ws.diag + 8 : nullptr;  // msg_set_diag: the round's wall-clock split (10 ns ticks)
+  const long long tk0 = dg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+  long long tw = 0, tc = 0;
+  int maxrec = 0;
   __syncthreads();
   while (!stop) {
     int r0 = 0;
@@ -182,7 +193,8 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
     const int j = r0 + lane;
     // ---- promote: final since the last round; their claims become permanent ----
     if (j < P) {
-      const int2 rc = ws.srec[(size_t)ppar * SPEC_WIN + j];
+      const int4 r4 = ws.srec[(size_t)ppar * SPEC_WIN + j];
+      const int2 rc = make_int2(r4.x, r4.y);
       ws.sfrec[j] = rc;
       for (int k = 0; k < rc.y; ++k) {
         const unsigned long long r = ws.slog[rc.x + k];
@@ -242,11 +254,12 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
         }
       }
     }
+    const long long tka = dg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
     // ---- wait for the earlier adjacent top pops of this round (lower ranks only) ----
     bool labd = !ex, pushd = !ex;
     int mylab = 0;
     unsigned pm = 0;
-    bool ovf = false;
+    bool ovf = false, cap = false;  // unstable; capacity overflow
     long long t0 = 0;
     int spins = 0;
     for (;;) {
@@ -323,99 +336,149 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
       }
     }
     if (stop) break;
-    if (!ex) continue;
-    // ---- the top pop's writes, then the cascade (levels < L, lowest first, FIFO) ----
-    claim_max(cur + p, spec_claim(T, j, 1u));
-    st_ag32(slc + p, mylab);
-    int nq = 0;
-    unsigned dm = 0;
-    if (mylab != WSHED) {
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        if (!((pm >> d) & 1u)) continue;
-        const int z = nbp[d];
-        claim_max(cur + z, spec_claim(T, j, 0u));
-        const unsigned t = (wp >> (8 * d)) & 255u;
-        if ((int)t < L) {
-          if (nq < SPEC_QCAP) lq[(nq++) * SPEC_BS + tid] = ((unsigned long long)t << 32) | (unsigned)z;
-          else ovf = true;
-        } else {
-          dm |= 1u << d;
-        }
-      }
-    }
-    unsigned long long rec = srec_pack(p, mylab, dm);
-    unsigned long long sig = smix(0x6a09e667f3bcc908ull, rec);
-    tmp[0] = rec;
-    int nrec = 1;
-    while (nq > 0 && !ovf) {
-      int bi = 0;
-      unsigned long long be = lq[tid];
-      for (int k = 1; k < nq; ++k) {
-        const unsigned long long e = lq[k * SPEC_BS + tid];
-        if ((e >> 32) < (be >> 32)) {
-          be = e;
-          bi = k;
-        }
-      }
-      for (int k = bi; k + 1 < nq; ++k) lq[k * SPEC_BS + tid] = lq[(k + 1) * SPEC_BS + tid];
-      --nq;
-      if (nrec >= SPEC_RL) {
-        ovf = true;
-        break;
-      }
-      const int y = (int)(uint32_t)be;
-      const unsigned wy = (unsigned)ws.w4[y];
-      const int yb = y + marg;
-      int nby[4], v[4];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) nby[d] = nbi(yb, d, Wt) - marg;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) v[d] = spec_view(ws, V, j, nby[d], true);
-      int lab = 0;
-#pragma unroll
-      for (int d = 0; d < 4; ++d)
-        if (v[d] > 0) lab = fold_lab(lab, v[d]);
-      if (lab == 0) {  // own writes hidden by a conflicting lower rank: unstable
-        ovf = true;
-        lab = WSHED;
-      }
-      claim_max(cur + y, spec_claim(T, j, 1u));
-      st_ag32(slc + y, lab);
-      unsigned dmy = 0;
-      if (lab != WSHED) {
-#pragma unroll
+    const long long tkb = dg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long sig = 0;
+    int nrec = 0;
+    if (ex) {
+      // ---- the top pop's writes, then the cascade (levels < L, lowest first, FIFO) ----
+      claim_max(cur + p, spec_claim(T, j, 1u));
+      st_ag32(slc + p, mylab);
+      int nq = 0;
+      unsigned dm = 0;
+      if (mylab != WSHED) {
+  #pragma unroll
         for (int d = 0; d < 4; ++d) {
-          if (v[d] != 0) continue;
-          const int z = nby[d];
+          if (!((pm >> d) & 1u)) continue;
+          const int z = nbp[d];
           claim_max(cur + z, spec_claim(T, j, 0u));
-          const unsigned t = (wy >> (8 * d)) & 255u;
+          const unsigned t = (wp >> (8 * d)) & 255u;
           if ((int)t < L) {
             if (nq < SPEC_QCAP) lq[(nq++) * SPEC_BS + tid] = ((unsigned long long)t << 32) | (unsigned)z;
-            else ovf = true;
+            else ovf = cap = true;
           } else {
-            dmy |= 1u << d;
+            dm |= 1u << d;
           }
         }
       }
-      rec = srec_pack(y, lab, dmy);
-      tmp[nrec++] = rec;
-      sig = smix(sig, rec);
+      unsigned long long rec = srec_pack(p, mylab, dm);
+      sig = smix(0x6a09e667f3bcc908ull, rec);
+      tmp[0] = rec;
+      nrec = 1;
+      while (nq > 0 && !ovf) {
+        if (nrec >= SPEC_RL) {
+          ovf = cap = true;
+          break;
+        }
+        int bi = 0;
+        unsigned long long be = lq[tid];
+        for (int k = 1; k < nq; ++k) {
+          const unsigned long long e = lq[k * SPEC_BS + tid];
+          if ((e >> 32) < (be >> 32)) {
+            be = e;
+            bi = k;
+          }
+        }
+        for (int k = bi; k + 1 < nq; ++k) lq[k * SPEC_BS + tid] = lq[(k + 1) * SPEC_BS + tid];
+        --nq;
+        const int y = (int)(uint32_t)be;
+        const unsigned wy = (unsigned)ws.w4[y];
+        const int yb = y + marg;
+        int nby[4], v[4];
+  #pragma unroll
+        for (int d = 0; d < 4; ++d) nby[d] = nbi(yb, d, Wt) - marg;
+  #pragma unroll
+        for (int d = 0; d < 4; ++d) v[d] = spec_view(ws, V, j, nby[d], true);
+        int lab = 0;
+  #pragma unroll
+        for (int d = 0; d < 4; ++d)
+          if (v[d] > 0) lab = fold_lab(lab, v[d]);
+        if (lab == 0) {  // own writes hidden by a conflicting lower rank: unstable
+          ovf = true;
+          lab = WSHED;
+        }
+        claim_max(cur + y, spec_claim(T, j, 1u));
+        st_ag32(slc + y, lab);
+        unsigned dmy = 0;
+        if (lab != WSHED) {
+  #pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            if (v[d] != 0) continue;
+            const int z = nby[d];
+            claim_max(cur + z, spec_claim(T, j, 0u));
+            const unsigned t = (wy >> (8 * d)) & 255u;
+            if ((int)t < L) {
+              if (nq < SPEC_QCAP) lq[(nq++) * SPEC_BS + tid] = ((unsigned long long)t << 32) | (unsigned)z;
+            else ovf = cap = true;
+            } else {
+              dmy |= 1u << d;
+            }
+          }
+        }
+        rec = srec_pack(y, lab, dmy);
+        tmp[nrec++] = rec;
+        sig = smix(sig, rec);
+      }
+    }  // ex
+    if (dg) {
+      tw += tkb - tka;
+      tc += (long long)__builtin_amdgcn_s_memrealtime() - tkb;
+      maxrec = max(maxrec, nrec);
     }
-    int base = 0;
-    if (!ovf) {
-      base = atomicAdd(&ctl->spec.logtop, nrec);
-      if ((long long)base + nrec > ws.slogcap) ovf = true;  // generation log full: unstable
-      else
-        for (int k = 0; k < nrec; ++k) ws.slog[base + k] = tmp[k];
+    // ---- log space for the wave's records (one atomic per wave), signatures, change words ----
+    const int want = (ex && !ovf) ? nrec : 0;
+    int incl = want;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
     }
-    sig = smix(sig, ((unsigned long long)nrec << 1) | (ovf ? 1ull : 0ull));
-    ws.srec[(size_t)par * SPEC_WIN + j] = make_int2(base, ovf ? 0 : nrec);
-    ws.ssig[(size_t)par * SPEC_WIN + j] = sig;
-    const bool changed = !V.hasprev || ovf || ws.ssig[(size_t)ppar * SPEC_WIN + j] != sig;
-    if (changed) atomicMin(&ctl->spec.fc, j);
-    if (ovf) atomicMin(&ctl->spec.ovfr, j);
-    atomicAdd(&s_exec, 1);
+    const int wtot = __shfl(incl, 63);
+    int wbase = 0;
+    if (lane == 0 && wtot) wbase = atomicAdd(&ctl->spec.logtop, wtot);
+    wbase = __shfl(wbase, 0);
+    int fcand = NONE, ocand = NONE;
+    if (ex) {
+      const int base = wbase + incl - want;
+      if (!ovf) {
+        if ((long long)base + nrec > ws.slogcap) ovf = cap = true;  // generation log full
+        else
+          for (int k = 0; k < nrec; ++k) ws.slog[base + k] = tmp[k];
+      }
+      sig = smix(sig, ((unsigned long long)nrec << 1) | (ovf ? 1ull : 0ull));
+      ws.srec[(size_t)par * SPEC_WIN + j] = make_int4(base, ovf ? 0 : nrec, (int)T, cap ? 1 : 0);
+      ws.ssig[(size_t)par * SPEC_WIN + j] = sig;
+      // unchanged = the same execution in the immediately preceding round
+      const bool changed = !V.hasprev || ovf || ws.srec[(size_t)ppar * SPEC_WIN + j].z != (int)(T - 1u) ||
+                           ws.ssig[(size_t)ppar * SPEC_WIN + j] != sig;
+      if (changed) fcand = j;
+      if (ovf) ocand = j;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      fcand = min(fcand, __shfl_xor(fcand, o));
+      ocand = min(ocand, __shfl_xor(ocand, o));
+    }
+    if (lane == 0) {
+      if (fcand != NONE) atomicMin(&ctl->spec.fc, fcand);
+      if (ocand != NONE) atomicMin(&ctl->spec.ovfr, ocand);
+      const int nex = max(0, min(n, r0 + 64) - max(P, r0));
+      if (nex) atomicAdd(&s_exec, nex);
+    }
+  }
+  if (dg) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) maxrec = max(maxrec, __shfl_xor(maxrec, o));
+    if (lane == 0) {
+      const long long tot = (long long)__builtin_amdgcn_s_memrealtime() - tk0;
+      atomicAdd(&dg[0], (unsigned long long)tw);  // wave time in the top-pop waits
+      atomicAdd(&dg[1], (unsigned long long)tc);  // wave time in top-pop writes + cascades
+      atomicAdd(&dg[2], (unsigned long long)tot); // wave time in the kernel
+      atomicMax(&dg[3], (unsigned long long)tot); // longest wave
+      atomicMax(&dg[4], (unsigned long long)maxrec);
+      atomicMax(&dg[6], (unsigned long long)tc);
+      atomicAdd(&dg[7], 1ull);
+      atomicMax(&ctl->spec.rmax, (unsigned long long)tot);
+    }
   }
   __syncthreads();
   if (tid == 0) {
@@ -423,7 +486,7 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
     __threadfence();
     if (atomicAdd(&ctl->spec.ticket, 1) == (int)gridDim.x - 1) {
       __threadfence();
-      spec_finalize(ctl, P, n, T, G);
+      spec_finalize(ctl, P, n, T, G, dg);
     }
   }
 }
@@ -478,7 +541,14 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
     if (tile >= ntiles) break;
     const int j = tile * SPEC_FT + tid;
     int2 rc = make_int2(0, 0);
-    if (j < P) rc = (j < Pprom) ? ws.sfrec[j] : ws.srec[(size_t)(T & 1u) * SPEC_WIN + j];
+    if (j < P) {
+      if (j < Pprom) {
+        rc = ws.sfrec[j];
+      } else {
+        const int4 r4 = ws.srec[(size_t)(T & 1u) * SPEC_WIN + j];
+        rc = make_int2(r4.x, r4.y);
+      }
+    }
     int x = rc.y;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -552,14 +622,29 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
       ctl->rsv = nb.epoch;
       s.gens += 1;
       s.cpops += Vn - P;
+      // every generation (fallbacks included) is judged against serial pops over the span since
+      // the regime's start: slower per committed pop (small generations: a round costs launch
+      // floors and its longest execution; frequent fallbacks) -> serial pops for a while
+      const long long el = (long long)__builtin_amdgcn_s_memrealtime() - s.tstart;
+      const long long done = ctl->pops + Vn - s.pstart;  // k_scan adds Vn after this kernel
+      ++s.accg;
+      const bool judge = s.accg >= SPEC_JUDGE_GENS || (s.accg >= 4 && el > SPEC_JUDGE_TICKS);
+      const bool slow = judge && el > (long long)SPEC_SERIAL_TICKS * done;
       if (s.fallback) {
         s.on = 0;
-        s.block = L;
+        s.block = slow ? 0 : L;
         s.fallbacks += 1;
         ctl->wcap = WMIN;
       } else if (Vn == P && s.n >= SPEC_QUIET) {  // a large generation without a cascade: batches pay
         s.on = 0;
         s.block = 0;
+      }
+      if (slow) {
+        s.on = 0;
+        s.block = 0;
+        s.cool = SPEC_COOL_POPS << min(s.fails, 6);
+        s.fails += 1;
+        s.fresh = 1;
       }
       s.state = 0;
       ctl->bat = nb;

@@ -1674,7 +1674,7 @@ __device__ __forceinline__ int lowest_bucket(const int* head, const int* tail, i
 
 __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qbase, int* s_head, int* s_tail,
                             int* s_wcap, int* s_err, int* s_nseg, int* s_n, int* s_ser, long long* cnt,
-                            int spec_block) {
+                            int spec_block, int* spec_cool) {
   const int lane = lane_id();
   const int Wt = ws.Wt, marg = ws.marg;
   const Batch B0 = *s_B;
@@ -1690,6 +1690,7 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
     }
     if (run >= SERIAL_RUN) break;
     if (spec_block > 0 && lo >= spec_block) break;  // the cascade that stopped the speculative engine is done
+    if (spec_cool && *spec_cool > 0 && pops >= *spec_cool) break;  // its cooldown is over
     if (lo != ring_l || h >= ring_h0 + ring_n) {  // the bucket's next 64 slots, one load per lane
       ring_l = lo;
       ring_h0 = h;
@@ -1748,6 +1749,7 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
     cnt[1] += pops;
     cnt[2] += pushes;
     *s_wcap = 0;  // the next batch: a whole generation (next_wcap shrinks it again on a cut)
+    if (spec_cool && *spec_cool > 0) *spec_cool = (int)max(0ll, (long long)*spec_cool - pops);
   }
   wave_sync();
   form_batch(s_qbase, s_head, s_tail, 0, 0, s_seg, s_nseg, s_n);
@@ -1781,6 +1783,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
   __shared__ int s_cut, s_segcut, s_minpush, s_err, s_nseg, s_n, s_wcap;
   __shared__ int s_ser;  // 1: the interrupt-dense regime, tiny batches popped serially
   __shared__ int s_specgo, s_specblk;  // hand the regime to the speculative engine; its resume level
+  __shared__ int s_specool;            // regime entries to skip first (SpecCtl.cool)
   __shared__ Batch s_B;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const int Wt = ws.Wt;
@@ -1791,6 +1794,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     s_ser = 0;
     s_specgo = 0;
     s_specblk = ws.scl ? ctl->spec.block : -1;  // -1: engine off
+    s_specool = ctl->spec.cool;
   }
   if (tid < NQ) {
     s_qbase[tid] = ctl->qbase[tid];
@@ -1810,14 +1814,17 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     if (B.n <= TINY_MAX) {  // runs of tiny batches: wave 0 alone, the other waves wait here
       if (wv == 0) {
         long long c4[4] = {0, 0, 0, 0};
-        if (s_ser && s_specblk >= 0 && lowest_bucket(s_head, s_tail, 0) >= s_specblk) {
+        if (s_ser && s_specblk >= 0 && s_specool <= 0 && lowest_bucket(s_head, s_tail, 0) >= s_specblk) {
           if (lane == 0) s_specgo = 1;  // interrupt-dense: speculative generations from here on
         } else if (s_ser) {
           serial_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, c4,
-                      s_specblk > 0 ? s_specblk : 0);
-          // the cascade that stopped the speculative engine is done: hand the regime back to it
-          // (not to a whole-bucket batch that the next interrupt cuts again)
-          if (s_specblk > 0 && s_B.n > 0 && lowest_bucket(s_head, s_tail, 0) >= s_specblk && lane == 0) s_specgo = 1;
+                      s_specblk > 0 ? s_specblk : 0, s_specblk >= 0 ? &s_specool : nullptr);
+          wave_sync();
+          // the cascade that stopped the speculative engine is done, or its cooldown is over:
+          // hand the regime back to it (not to a whole-bucket batch the next interrupt cuts again)
+          if (s_specblk >= 0 && s_specool <= 0 && s_B.n > 0 && lowest_bucket(s_head, s_tail, 0) >= s_specblk &&
+              lane == 0)
+            s_specgo = 1;
         } else
           tiny_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, s_wcnt[0], &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, c4);
         if (tid == 0) {
@@ -2007,11 +2014,18 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     Batch nb = s_B;
     if (s_specgo) {
       spec_begin(ctl, nb, nb.L, s_qbase[nb.L] + s_head[nb.L], s_tail[nb.L] - s_head[nb.L]);
+      if (ctl->spec.fresh || ctl->spec.tstart == 0) {  // flood start, or after a cooldown: judge anew
+        ctl->spec.fresh = 0;
+        ctl->spec.accg = 0;
+        ctl->spec.tstart = (long long)__builtin_amdgcn_s_memrealtime();
+        ctl->spec.pstart = ctl->pops + nb_pops;  // nb_pops: this loop's, added below
+      }
       ctl->spec.on = 1;
       ctl->spec.block = 0;
     }
     ctl->bat = nb;
     ctl->wcap = s_wcap;
+    ctl->spec.cool = s_specool;
     ctl->cut = NONE;
     ctl->segcut = NONE;
     ctl->minpush = NQ;

@@ -70,6 +70,12 @@ constexpr int SPEC_RL = 256;        // records per execution (lane scratch): mor
 constexpr int SPEC_ROUNDS_MAX = 64; // rounds per generation before the stable prefix is committed
 constexpr int SPEC_FT = 1024;       // items per k_spec_flatten tile
 constexpr int SPEC_QUIET = 4096;    // a generation this large without a cascade ends the regime
+constexpr int SPEC_SERIAL_TICKS = 50;        // ~0.5 us per serial pop (10 ns ticks): a regime
+constexpr int SPEC_JUDGE_GENS = 16;          // slower than that per committed pop (its fallbacks'
+                                             // serial pops included), after this many
+                                             // generations, ends for
+constexpr int SPEC_COOL_POPS = 65536;        // this many serial pops (doubling per repeat)
+constexpr int SPEC_JUDGE_TICKS = 200000;     // slow generations are judged after 4 once 2 ms passed
 
 struct SpecCtl {
   unsigned T;     // current round tag: round claims in scl[T & 1], labels in slab[T & 1]
@@ -89,8 +95,13 @@ struct SpecCtl {
   int logtop;     // generation log records used
   int fallback;   // the commit ends the regime (overflow at the stable prefix)
   int ftile;      // k_spec_flatten tile dealing
-  int pad;
+  int cool;       // serial pops to go before the regime may start again
+  int accg;       // generations since the regime started (fallback resumptions included)
+  int fails;      // times the regime ended for being slower than serial pops
+  int fresh;      // the next start opens a new judging span (flood start, after such an end)
+  long long tstart, pstart;  // regime start: s_memrealtime, Ctl.pops
   long long gens, rounds_total, execs, cpops, fallbacks;
+  unsigned long long rmax;  // diagnostics: longest wave of this round (10 ns ticks)
 };
 
 // desc word of a batch item: bits 0-31 the 4 edge weights, 32-35 push (or 0-neighbour) mask,
@@ -172,7 +183,7 @@ struct Ws {
   int32_t* slab;             // 2 x snp labels of popped pixels
   unsigned long long* stl;   // SPEC_WIN top-pop granules {round tag, label}
   unsigned long long* slog;  // generation log: records {label, dmask, pixel}
-  int2* srec;                // 2 x SPEC_WIN {log base, records} per round parity
+  int4* srec;                // 2 x SPEC_WIN {log base, records, round tag, capacity overflow} per round parity
   unsigned long long* ssig;  // 2 x SPEC_WIN execution signatures
   int2* sfrec;               // SPEC_WIN {log base, records} of promoted items
   unsigned long long* stmp;  // lane scratch: SPEC_RL records per k_spec_round thread

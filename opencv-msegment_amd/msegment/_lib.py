@@ -23,6 +23,11 @@ MSG_ERANGE = -6
 
 MSG_NC_GISTO_DIAP = 0x1
 MSG_NC_MULTI_OTSU = 0x2
+MSG_NC_MEDIAN_BLUR = 0x4
+
+
+def MSG_NC_MASK(k):
+    return (int(k) & 0xff) << 8
 
 # every symbol include/msegment.h declares (checked by tests/test_abi.py)
 EXPORTS = (

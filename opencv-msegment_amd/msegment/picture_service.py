@@ -61,13 +61,15 @@ class PictureService:
         depth = int(depth)
         return self.segmenter.colorize(markers, depth, self._palette(depth, colored))
 
-    def not_connected_markers(self, src, depth, options=(), colored_markers=False):
+    def not_connected_markers(self, src, depth, options=(), colored_markers=False, filter_mask_size=3):
         """PictureService.notConnectedMarkers (PictureService.java:468-867) on the GPU.
 
         ``options``: names of AlgorithmOptions (model/dic/AlgorithmOptions.java).  COLORED,
-        GISTO_DIAP and MULTI_OTSU change the result; NO_SAVE_STEPS / BW_RESULT only concern
-        saving step images, which is not part of this drop-in (every step image is skipped).
-        MEDIAN_BLUR / BILATERIAL (:481-495) raise MsegError(EINVAL): not built yet.
+        GISTO_DIAP, MULTI_OTSU and MEDIAN_BLUR change the result; NO_SAVE_STEPS / BW_RESULT only
+        concern saving step images, which is not part of this drop-in (every step image is
+        skipped).  MEDIAN_BLUR = medianBlur(srcGray, filter_mask_size) before the histogram
+        (:481-483; an even size raises MsegError(EINVAL), like medianBlur's assertion).
+        BILATERIAL (:487-494, a floating-point bilateralFilter) raises MsegError(EINVAL).
 
         Same Random draws as the reference: colorByIndexes(markers, n, true) for the
         "colored_markers_summ" step (:830) draws n colours before the watershed's own
@@ -81,10 +83,12 @@ class PictureService:
         from . import MsegError, _lib
 
         opts = set(options)
-        if opts & {"MEDIAN_BLUR", "BILATERIAL"}:
-            raise MsegError(_lib.MSG_EINVAL, "MEDIAN_BLUR / BILATERIAL pre-filters not supported")
+        if "BILATERIAL" in opts and "MEDIAN_BLUR" not in opts:  # MEDIAN_BLUR wins (if / else if)
+            raise MsegError(_lib.MSG_EINVAL, "BILATERIAL pre-filter not supported")
         flags = (_lib.MSG_NC_GISTO_DIAP if "GISTO_DIAP" in opts else 0) | (
             _lib.MSG_NC_MULTI_OTSU if "MULTI_OTSU" in opts else 0)
+        if "MEDIAN_BLUR" in opts:
+            flags |= _lib.MSG_NC_MEDIAN_BLUR | _lib.MSG_NC_MASK(filter_mask_size)
         colored = "COLORED" in opts
         src = np.ascontiguousarray(np.asarray(src, dtype=np.uint8))
         H, W = src.shape[:2]

@@ -228,9 +228,14 @@ def markers(gray_img, lut):
     return lut[np.asarray(gray_img)].astype(np.int32)
 
 
-def marker_stage(bgr, depth, gisto_diap=False, multi_otsu_opt=False):
-    """gray, hist, levels, markers of one BGR frame."""
+def marker_stage(bgr, depth, gisto_diap=False, multi_otsu_opt=False, median_blur=0):
+    """gray, hist, levels, markers of one BGR frame.  median_blur = k > 0: the MEDIAN_BLUR branch
+    (PictureService.java:481-483), medianBlur(srcGray, k) before the histogram (restated as the
+    exact k x k median with replicated borders, oracle/shape_oracle.median)."""
     g = gray(bgr)
+    if median_blur:
+        from oracle import shape_oracle
+        g = shape_oracle.median(g, int(median_blur))
     h = hist256(g)
     lv = levels(h, bgr.shape[0], bgr.shape[1], depth, gisto_diap, multi_otsu_opt)
     return g, h, lv, markers(g, marker_lut(lv, gisto_diap))

@@ -43,11 +43,16 @@ def named(names):
 def main():
     quick = len(sys.argv) > 1 and sys.argv[1] == "quick"
     prof = "prof" in sys.argv
-    sel = [a for a in sys.argv[1:] if a not in ("quick", "prof")]
+    sel = [a for a in sys.argv[1:] if a not in ("quick", "prof", "album")]
+    if "album" in sys.argv:
+        sel = None
     seg = msegment.Segmenter(0)
     dev = torch.device("cuda", 0)
     bad = 0
-    for name, img, m in (named(sel) if sel else frames(quick)):
+    todo = named(sel) if sel else frames(quick)
+    if sel is None:
+        todo = [f for f in frames(False) if f[0].startswith("album")]
+    for name, img, m in todo:
         if m is None:
             m = np.ascontiguousarray(seg.shape_markers(img)[0])
         want = ws_oracle.watershed(img, m)

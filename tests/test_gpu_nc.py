@@ -86,6 +86,32 @@ def test_marker_stage_matches_oracle(seg, opts, kind, shape, depth):
     assert np.array_equal(m2.cpu().numpy(), mk)
 
 
+@pytest.mark.parametrize("k", [1, 3, 5, 9, 15])
+@pytest.mark.parametrize("kind,shape", [("mosaic_noise", (211, 307)), ("random", (64, 96))])
+def test_marker_stage_median_blur(seg, k, kind, shape):
+    """MEDIAN_BLUR (PictureService.java:481-483): medianBlur(srcGray, k), then histogram, levels
+    and markers from the blurred gray."""
+    torch = _torch()
+    img, _, _ = synth.frame(kind, shape[0], shape[1], 9)
+    g, h, lv, mk = O.marker_stage(img, 4, median_blur=k)
+    m = torch.empty(shape, dtype=torch.int32, device="cuda:0")
+    gray = torch.empty(shape, dtype=torch.uint8, device="cuda:0")
+    got = seg.nc_marker_stage_dev(_dev(img), 4, m, _lib.MSG_NC_MEDIAN_BLUR | _lib.MSG_NC_MASK(k), gray=gray)
+    torch.cuda.synchronize()
+    assert np.array_equal(gray.cpu().numpy(), g)
+    assert got == lv
+    assert np.array_equal(m.cpu().numpy(), mk)
+
+
+def test_marker_stage_median_blur_even_mask(seg):
+    torch = _torch()
+    img, _, _ = synth.frame("mosaic_noise", 32, 32, 9)
+    m = torch.empty((32, 32), dtype=torch.int32, device="cuda:0")
+    with pytest.raises(msegment.MsegError) as e:
+        seg.nc_marker_stage_dev(_dev(img), 4, m, _lib.MSG_NC_MEDIAN_BLUR | _lib.MSG_NC_MASK(4))
+    assert e.value.code == _lib.MSG_EINVAL
+
+
 def test_marker_stage_multi_otsu(seg):
     torch = _torch()
     # three flat patches -> three flex levels -> the multi-Otsu override (k = 3)
@@ -114,10 +140,11 @@ def test_marker_stage_errors(seg):
     assert e.value.code == _lib.MSG_EINVAL
 
 
-def _oracle_nc(img, depth, opts, seed):
+def _oracle_nc(img, depth, opts, seed, mask=3):
     """notConnectedMarkers end to end on the CPU oracles, with the reference's Random draws."""
     gisto, otsu, colored = "GISTO_DIAP" in opts, "MULTI_OTSU" in opts, "COLORED" in opts
-    g, h, lv, mk = O.marker_stage(img, depth, gisto_diap=gisto, multi_otsu_opt=otsu)
+    g, h, lv, mk = O.marker_stage(img, depth, gisto_diap=gisto, multi_otsu_opt=otsu,
+                                  median_blur=mask if "MEDIAN_BLUR" in opts else 0)
     n = len(lv)
     rnd = JavaRandom(seed)
     draw = lambda: [rnd.next_int(156) + 100 for _ in range(3)]  # noqa: E731
@@ -128,12 +155,13 @@ def _oracle_nc(img, depth, opts, seed):
     return dst, ws_oracle.bgr2gray(dst), labels, lv, ws_oracle.colorize(mk, n, step_pal)
 
 
-@pytest.mark.parametrize("opts", [("COLORED",), ("COLORED", "GISTO_DIAP"), ()])
+@pytest.mark.parametrize("opts", [("COLORED",), ("COLORED", "GISTO_DIAP"), (), ("MEDIAN_BLUR", "COLORED"),
+                                  ("MEDIAN_BLUR", "BILATERIAL")])
 def test_not_connected_markers_pipeline(opts):
     img, _, _ = synth.frame("mosaic_noise", 192, 160, 11)
     ps = msegment.PictureService(seed=2024)
-    r = ps.not_connected_markers(img, 4, opts, colored_markers=True)
-    dst, bw, labels, lv, cm = _oracle_nc(img, 4, opts, 2024)
+    r = ps.not_connected_markers(img, 4, opts, colored_markers=True, filter_mask_size=5)
+    dst, bw, labels, lv, cm = _oracle_nc(img, 4, opts, 2024, mask=5)
     assert r.levels == lv
     assert np.array_equal(r.labels, labels)
     assert np.array_equal(r.colored_markers, cm)
@@ -176,3 +204,10 @@ def test_host_buffer_marker_stage(seg):
     with pytest.raises(msegment.MsegError) as e:
         seg.nc_marker_stage(np.full((4, 4, 3), 255, np.uint8), 3)
     assert e.value.code == _lib.MSG_ESTATE
+
+
+def test_not_connected_markers_bilateral_rejected():
+    img, _, _ = synth.frame("mosaic_noise", 32, 32, 11)
+    with pytest.raises(msegment.MsegError) as e:
+        msegment.PictureService(seed=1).not_connected_markers(img, 4, ("BILATERIAL",))
+    assert e.value.code == _lib.MSG_EINVAL

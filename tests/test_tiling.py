@@ -13,6 +13,8 @@ HDR = os.path.join(ROOT, "opencv-msegment_amd", "csrc", "ws_shared.h")
 DRIVER = r'''
 #define __host__
 #define __device__
+struct int2 { int x, y; };  // HIP vector types used by the header's workspace pointers
+struct int4 { int x, y, z, w; };
 #include <cstdio>
 #include <cstdlib>
 #include <initializer_list>
