@@ -724,7 +724,12 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
     // depend on how many of the blocks are resident (msg_set_resolve_grid overrides it)
     c->res_grid = cus * std::max(1, std::min(per, 4));
     c->cus = cus;
-    c->spec_grid = 2 * cus;  // k_spec_round: 64 KB of LDS cascade queues per block, two per CU
+    // k_spec_round: as many blocks as fit at once (LDS cascade queues, VGPRs); ranks are dealt
+    // in dispatch order, so this is a performance choice only
+    int sper = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&sper, k_spec_round, SPEC_BS, 0) != hipSuccess || sper <= 0)
+      sper = 1;
+    c->spec_grid = cus * sper;
   }
   *out = c;
   return MSG_OK;

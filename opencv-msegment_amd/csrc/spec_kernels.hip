@@ -631,6 +631,9 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
       const bool judge = s.accg >= SPEC_JUDGE_GENS || (s.accg >= 4 && el > SPEC_JUDGE_TICKS);
       const bool slow = judge && el > (long long)SPEC_SERIAL_TICKS * done;
       if (s.fallback) {
+        // the batch engine pops the overflowing item and its cascade (serial pops); the regime
+        // resumes once the lowest level is back at L (generations inside a cascade that
+        // overflowed a lane are small: measured slower)
         s.on = 0;
         s.block = slow ? 0 : L;
         s.fallbacks += 1;

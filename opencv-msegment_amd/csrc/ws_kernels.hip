@@ -1680,6 +1680,7 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
   const Batch B0 = *s_B;
   long long pops = 0, pushes = 0;
   int run = 0;
+  const long long cool_lim = (spec_cool && *spec_cool > 0) ? *spec_cool : (1ll << 62);
   int lo = lowest_bucket(s_head, s_tail, 0);
   int ring = 0, ring_l = -1, ring_h0 = 0, ring_n = 0;
   while (lo < NQ) {
@@ -1690,7 +1691,7 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
     }
     if (run >= SERIAL_RUN) break;
     if (spec_block > 0 && lo >= spec_block) break;  // the cascade that stopped the speculative engine is done
-    if (spec_cool && *spec_cool > 0 && pops >= *spec_cool) break;  // its cooldown is over
+    if (pops >= cool_lim) break;  // its cooldown is over
     if (lo != ring_l || h >= ring_h0 + ring_n) {  // the bucket's next 64 slots, one load per lane
       ring_l = lo;
       ring_h0 = h;

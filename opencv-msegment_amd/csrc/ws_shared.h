@@ -65,8 +65,14 @@ constexpr int ERR_CAPACITY = 4;
 // changes (the serial result is the unique fixed point: item i depends only on items < i).
 constexpr int SPEC_WIN = 1 << 20;   // items per generation (claim ranks have 22 bits)
 constexpr int SPEC_BS = 256;        // threads per k_spec_round block
-constexpr int SPEC_QCAP = 32;       // per-lane cascade queue (LDS): more live entries = overflow
-constexpr int SPEC_RL = 256;        // records per execution (lane scratch): more = overflow
+#ifndef MSEG_SPEC_QCAP
+#define MSEG_SPEC_QCAP 32
+#endif
+#ifndef MSEG_SPEC_RL
+#define MSEG_SPEC_RL 256
+#endif
+constexpr int SPEC_QCAP = MSEG_SPEC_QCAP;  // per-lane cascade queue (LDS): more live entries = overflow
+constexpr int SPEC_RL = MSEG_SPEC_RL;      // records per execution (lane scratch): more = overflow
 constexpr int SPEC_ROUNDS_MAX = 64; // rounds per generation before the stable prefix is committed
 constexpr int SPEC_FT = 1024;       // items per k_spec_flatten tile
 constexpr int SPEC_QUIET = 4096;    // a generation this large without a cascade ends the regime

@@ -32,10 +32,16 @@ def frames(quick):
 
 
 def named(names):
+    """kind_S_sSEED frames; an "nc_" prefix replaces the seeds by the NC pipeline's marker map
+    (depth 4, GISTO_DIAP: every pixel whose gray is a level's mean band is a seed)."""
     out = []
     for nm in names:
-        kind, S, seed = nm.rsplit("_", 2)
+        nc = nm.startswith("nc_")
+        kind, S, seed = (nm[3:] if nc else nm).rsplit("_", 2)
         img, m, _ = synth.frame(kind, int(S), int(S), int(seed[1:]))
+        if nc:
+            from oracle import nc_oracle
+            m = np.ascontiguousarray(nc_oracle.marker_stage(img, 4, gisto_diap=True)[3])
         out.append((nm, img, m))
     return out
 
