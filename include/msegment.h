@@ -69,7 +69,7 @@ typedef struct msg_stats {
     int64_t spec_fallbacks;     /* overflowing executions handed to serial pops                 */
 } msg_stats;
 
-#define MSG_NKERNELS 20
+#define MSG_NKERNELS 21
 typedef struct msg_kernel_profile {
     char    name[32];       /* kernel name, e.g. "k_resolve"                                   */
     int64_t launches;       /* launches timed since the last reset                              */
@@ -251,6 +251,31 @@ int msg_shape_markers_dev(msg_ctx* ctx, const void* d_bgr, int rows, int cols, i
 /* Host-buffer form (synchronous; strides in bytes). */
 int msg_shape_markers(msg_ctx* ctx, const uint8_t* bgr, size_t bgr_stride, int rows, int cols,
                       int ksize, int32_t* markers, size_t marker_stride, int* depth, int* ncomp);
+
+/* ---- COLOR_METHOD marker stage: the caller that builds the flood's seeds in
+ * PictureService.colorAutoMarkerWatershed (PictureService.java:301-392):
+ *   white -> black, src - filter2D(9x1 Laplacian column) saturated = the flood's src (:308-333)
+ *   -> bw = threshold(BGR2GRAY, OTSU) (:338, :938-943)
+ *   -> distanceTransform(bw, DIST_L2, 5), normalize(NORM_MINMAX) (:343, :1018-1023)
+ *   -> threshold(0.4), dilate 3x3 (:348-350)
+ *   -> findContours(RETR_CCOMP) + drawContours(i, i + 1, FILLED, hierarchy) + circle((5,5), 3,
+ *      255) = the markers, depth = the contour count (:355-365)
+ * Then msg_watershed_colorize*(sharp, markers, depth, ...) is the reference's this.watershed
+ * (:378).  The contour numbering is restated through connected components:
+ * unpinned against a real OpenCV build, like the rest of the stage.
+ * ----------------------------------------------------------------------------------------- */
+
+/* The whole stage on device buffers: d_bgr (rows*cols*3, BGR) in; d_sharp (rows*cols*3, the
+ * sharpened BGR image the watershed floods) and d_markers (int32 rows*cols) out; *depth (host)
+ * = the contour count.  d_bgr and d_sharp must not alias.  Returns when depth is known (the
+ * outputs are complete on `stream`). */
+int msg_color_markers_dev(msg_ctx* ctx, const void* d_bgr, int rows, int cols, void* d_sharp,
+                          void* d_markers, int* depth, void* stream);
+
+/* Host-buffer form (synchronous; strides in bytes). */
+int msg_color_markers(msg_ctx* ctx, const uint8_t* bgr, size_t bgr_stride, int rows, int cols,
+                      uint8_t* sharp, size_t sharp_stride, int32_t* markers, size_t marker_stride,
+                      int* depth);
 
 #ifdef __cplusplus
 }

@@ -24,6 +24,7 @@
 #include "spec_kernels.hip"
 #include "nc_kernels.hip"
 #include "shape_kernels.hip"
+#include "color_kernels.hip"
 
 #include <hipcub/hipcub.hpp>
 
@@ -103,19 +104,27 @@ struct msg_ctx {
   int *d_shF = nullptr, *d_shP = nullptr, *d_shcnt = nullptr;
   void* d_scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
+  // colour marker stage: 5 int planes (distances, fg / bg components, region labels x 2), the
+  // region lists, sweep flags and counters
+  long long cm_n = 0;
+  int* d_cm32 = nullptr;
+  int2* d_cmreg = nullptr;
+  int* d_cmcnt = nullptr;
 };
 
 namespace {
 
 enum KernelId { KID_PREP, KID_INIT_SCAN, KID_COMPACT, KID_RESOLVE, KID_SCAN, KID_SCATTER,
                 KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_GRAY_HIST, KID_NC_MARKERS, KID_SPEC_ROUND,
-                KID_GRAY, KID_MEDIAN, KID_CANNY, KID_CCL, KID_RING, KID_NUMBER, KID_HOLES, KID_SPEC_FLATTEN };
+                KID_GRAY, KID_MEDIAN, KID_CANNY, KID_CCL, KID_RING, KID_NUMBER, KID_HOLES, KID_SPEC_FLATTEN,
+                KID_COLOR };
 const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_compact", "k_resolve",
                                                 "k_scan", "k_scatter", "k_colorize",
                                                 "k_edge_weights", "k_untile", "k_gray_hist",
                                                 "k_nc_markers", "k_spec_round", "k_gray",
                                                 "k_median", "k_canny_nms", "k_ccl", "k_ring_median3",
-                                                "k_cc_number", "k_holes", "k_spec_flatten"};
+                                                "k_cc_number", "k_holes", "k_spec_flatten",
+                                                "k_color_stage"};
 
 hipEvent_t pool_event(msg_ctx* c) {
   if (c->evused == c->evpool.size()) {
@@ -672,6 +681,44 @@ int ensure_shape(msg_ctx* c, long long N, long long nb) {
   return MSG_OK;
 }
 
+int ensure_color(msg_ctx* c, long long N) {
+  if (c->cm_n >= N) return MSG_OK;
+  dfree(c->d_cm32);
+  dfree(c->d_cmreg);
+  c->cm_n = 0;
+  HIPCHK(c, hipMalloc((void**)&c->d_cm32, 5 * N * sizeof(int) + 64));
+  HIPCHK(c, hipMalloc((void**)&c->d_cmreg, 2 * N * sizeof(int2) + 64));
+  if (!c->d_cmcnt) HIPCHK(c, hipMalloc((void**)&c->d_cmcnt, 16 * sizeof(int)));
+  c->cm_n = N;
+  return MSG_OK;
+}
+
+// OpenCV's getThreshVal_Otsu_8u (threshold(..., THRESH_OTSU), PictureService.java:941): the first
+// threshold of maximal between-class variance, in double arithmetic, operation for operation.
+double otsu_threshold(const int32_t* h, long long n) {
+  const double scale = 1.0 / (double)n;
+  double mu = 0;
+  for (int i = 0; i < 256; ++i) mu += i * (double)h[i];
+  mu *= scale;
+  double mu1 = 0, q1 = 0, max_sigma = 0, max_val = 0;
+  const double eps = 1.1920928955078125e-07;  // FLT_EPSILON
+  for (int i = 0; i < 256; ++i) {
+    const double p_i = h[i] * scale;
+    mu1 *= q1;
+    q1 += p_i;
+    const double q2 = 1. - q1;
+    if (std::min(q1, q2) < eps || std::max(q1, q2) > 1. - eps) continue;
+    mu1 = (mu1 + i * p_i) / q1;
+    const double mu2 = (mu - q1 * mu1) / q2;
+    const double sigma = q1 * q2 * (mu1 - mu2) * (mu1 - mu2);
+    if (sigma > max_sigma) {
+      max_sigma = sigma;
+      max_val = i;
+    }
+  }
+  return max_val;
+}
+
 // Union-find labelling of the pixels `mode` selects (k_ccl_*): L = root per pixel, -1 elsewhere.
 int ccl(msg_ctx* c, const uint8_t* a, int* L, int H, int W, int mode, hipStream_t st) {
   const long long N = (long long)H * W;
@@ -756,6 +803,9 @@ void msg_destroy(msg_ctx* c) {
   dfree(c->d_shP);
   dfree(c->d_shcnt);
   dfree(c->d_scan_tmp);
+  dfree(c->d_cm32);
+  dfree(c->d_cmreg);
+  dfree(c->d_cmcnt);
   if (c->h_hist) (void)hipHostFree(c->h_hist);
   if (c->h_mir) (void)hipHostFree(c->h_mir);
   for (auto& e : c->evpool) (void)hipEventDestroy(e);
@@ -1262,6 +1312,241 @@ int msg_shape_markers_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, int
   if (c->prof) collect_profile(c);
   *ncomp = tailv[0] + tailv[1];
   *depth = *ncomp + holes;
+  return MSG_OK;
+}
+
+int msg_color_markers_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, void* d_sharp,
+                          void* d_markers, int* depth, void* stream) {
+  if (!c) return MSG_EINVAL;
+  int rc = check_size(c, rows, cols);
+  if (rc) return rc;
+  if (!depth) return fail(c, MSG_EINVAL, "null depth pointer");
+  *depth = 0;
+  const long long N = (long long)rows * cols;
+  if (N == 0) return MSG_OK;
+  if (!d_bgr || !d_sharp || !d_markers) return fail(c, MSG_EINVAL, "null device pointer");
+  if (d_bgr == d_sharp) return fail(c, MSG_EINVAL, "d_sharp must not alias d_bgr");
+  if (!aligned(d_sharp, 4)) return fail(c, MSG_EINVAL, "d_sharp must be 4-byte aligned");
+  HIPCHK(c, hipSetDevice(c->dev));
+  StreamScope scope(c, stream);
+  if (scope.rc) return scope.rc;
+  hipStream_t st = scope.st;
+  const int H = rows, W = cols;
+  rc = ensure_shape(c, N, 1);
+  if (rc) return rc;
+  rc = ensure_color(c, N);
+  if (rc) return rc;
+  uint8_t* gray = c->d_sh8;
+  uint8_t* thr = gray + N;
+  uint8_t* pk = thr + N;
+  uint8_t* frame = pk + N;
+  unsigned* dt = (unsigned*)c->d_cm32;
+  int* L = c->d_cm32 + N;
+  int* L2 = L + N;
+  int* R1 = L2 + N;
+  int* R2 = R1 + N;
+  int2* comps = c->d_cmreg;
+  int2* holes = comps + N;
+  int* cnt = c->d_cmcnt;  // [0,1] region counts, [2,3] min/max distance, [8..15] sweep flags
+  const int grid = stream_grid(N);
+  const dim3 rowg((W + 255) / 256, H);
+  uint8_t* sharp = (uint8_t*)d_sharp;
+  LAUNCH(c, KID_COLOR, st, k_cm_sharpen, rowg, dim3(256), 0, (const uint8_t*)d_bgr, sharp, H, W);
+  HIPCHK(c, hipGetLastError());
+  int32_t hist[256];
+  rc = gray_hist(c, sharp, N, gray, hist, st);  // bwMat: cvtColor(BGR2GRAY) + its histogram
+  if (rc) return rc;
+  const int t = (int)otsu_threshold(hist, N);
+  LAUNCH(c, KID_COLOR, st, k_cm_dt_init, dim3(grid), dim3(256), 0, gray, t, dt, N);
+  // chamfer distance: relaxation sweeps until one changes nothing (flags checked per 8 sweeps)
+  int flags[8];
+  const int max_sweeps = H + W + 16;
+  bool done = false;
+  for (int s0 = 0; s0 < max_sweeps && !done; s0 += 8) {
+    HIPCHK(c, hipMemsetAsync(cnt + 8, 0, 8 * sizeof(int), st));
+    for (int k = 0; k < 8; ++k) LAUNCH(c, KID_COLOR, st, k_cm_dt_sweep, rowg, dim3(256), 0, dt, H, W, cnt + 8 + k);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(flags, cnt + 8, sizeof(flags), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    for (int k = 0; k < 8; ++k) done = done || flags[k] == 0;
+  }
+  if (!done) return fail(c, MSG_ESTATE, "distance transform did not converge");
+  // normalize(NORM_MINMAX): min / max of the float distances (monotone in the fixed point)
+  unsigned mm[2] = {0xffffffffu, 0};
+  HIPCHK(c, hipMemcpyAsync(cnt + 2, mm, sizeof(mm), hipMemcpyHostToDevice, st));
+  LAUNCH(c, KID_COLOR, st, k_cm_minmax, dim3(grid), dim3(256), 0, dt, N, (unsigned*)(cnt + 2));
+  HIPCHK(c, hipMemcpyAsync(mm, cnt + 2, sizeof(mm), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  const float dlo = (float)mm[0] * (1.0f / 65536.0f), dhi = (float)mm[1] * (1.0f / 65536.0f);
+  float scf = 0.f, shf = 0.f;
+  int use_shift = 0;
+  if ((double)dhi - (double)dlo > 2.220446049250313e-16) {
+    const double sc = 1.0 / ((double)dhi - (double)dlo);
+    scf = (float)sc;
+    shf = (float)(-(double)dlo * sc);
+    use_shift = dlo != 0.f;
+  }
+  LAUNCH(c, KID_COLOR, st, k_cm_peaks, dim3(grid), dim3(256), 0, dt, scf, shf, use_shift, thr, N);
+  LAUNCH(c, KID_COLOR, st, k_cm_dilate3, rowg, dim3(256), 0, thr, pk, H, W);
+  HIPCHK(c, hipGetLastError());
+  // contours through components: foreground 8-connected, background 4-connected, holes = the
+  // background components that do not touch the frame
+  rc = ccl(c, pk, L, H, W, 1, st);
+  if (rc) return rc;
+  rc = ccl(c, pk, L2, H, W, 2, st);
+  if (rc) return rc;
+  HIPCHK(c, hipMemsetAsync(frame, 0, N, st));
+  LAUNCH(c, KID_HOLES, st, k_hole_border, dim3(std::max(1, (int)((2ll * W + 2ll * H + 255) / 256))), dim3(256), 0,
+         L2, frame, H, W);
+  HIPCHK(c, hipMemsetAsync(cnt, 0, 2 * sizeof(int), st));
+  LAUNCH(c, KID_COLOR, st, k_cm_regions, dim3(grid), dim3(256), 0, pk, L, L2, frame, W, N, comps, holes, cnt);
+  HIPCHK(c, hipGetLastError());
+  int nreg[2];
+  HIPCHK(c, hipMemcpyAsync(nreg, cnt, sizeof(nreg), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  const int nc = nreg[0], nh = nreg[1];
+  std::vector<int2> hc(nc), hh(nh);
+  if (nc) HIPCHK(c, hipMemcpyAsync(hc.data(), comps, nc * sizeof(int2), hipMemcpyDeviceToHost, st));
+  if (nh) HIPCHK(c, hipMemcpyAsync(hh.data(), holes, nh * sizeof(int2), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  // RETR_CCOMP order: components (outer borders, discovered at their first pixel) in reverse
+  // discovery order, each followed by its holes (discovered left of their first pixel) in
+  // reverse discovery order -- cvInsertNodeIntoTree prepends, cvTreeToNodeSeq walks depth-first
+  std::sort(hc.begin(), hc.end(), [](const int2& a, const int2& b) { return a.x > b.x; });
+  std::sort(hh.begin(), hh.end(), [](const int2& a, const int2& b) { return a.x > b.x; });
+  std::vector<std::pair<int, int>> cidx;  // (root, index)
+  std::vector<std::pair<int, int>> hidx;
+  {
+    // holes grouped by parent component root, already in descending key order
+    std::vector<std::pair<int, int>> byparent(nh);  // (parent root, position in hh)
+    for (int k = 0; k < nh; ++k) byparent[k] = {hh[k].y, k};
+    std::stable_sort(byparent.begin(), byparent.end(),
+                     [](const std::pair<int, int>& a, const std::pair<int, int>& b) { return a.first < b.first; });
+    int idx = 0;
+    cidx.reserve(nc);
+    hidx.reserve(nh);
+    for (int k = 0; k < nc; ++k) {
+      const int r = hc[k].x;
+      cidx.push_back({r, idx++});
+      auto lo = std::lower_bound(byparent.begin(), byparent.end(), std::make_pair(r, -1));
+      for (auto it = lo; it != byparent.end() && it->first == r; ++it) hidx.push_back({hh[it->second].x, idx++});
+    }
+    if ((int)hidx.size() != nh) return fail(c, MSG_ESTATE, "a hole without its component");
+  }
+  *depth = nc + nh;
+  // covering labels: 1 + the highest index among the contours whose fill covers a region
+  std::vector<std::pair<int, int>> hinfo(nh);  // sorted by root: (root, position in hidx)
+  for (int k = 0; k < nh; ++k) hinfo[k] = {hidx[k].first, k};
+  std::sort(hinfo.begin(), hinfo.end());
+  std::vector<std::pair<int, int>> cinfo(nc);
+  for (int k = 0; k < nc; ++k) cinfo[k] = {cidx[k].first, k};
+  std::sort(cinfo.begin(), cinfo.end());
+  auto hpos = [&](int root) -> int {
+    auto it = std::lower_bound(hinfo.begin(), hinfo.end(), std::make_pair(root, -1));
+    return (it != hinfo.end() && it->first == root) ? it->second : -1;
+  };
+  auto cpos = [&](int root) -> int {
+    auto it = std::lower_bound(cinfo.begin(), cinfo.end(), std::make_pair(root, -1));
+    return (it != cinfo.end() && it->first == root) ? it->second : -1;
+  };
+  std::vector<int> cenc(nc, -2);  // highest index among the holes enclosing component k
+  std::vector<int> hpar(nh), cholepar(nc);
+  for (int k = 0; k < nh; ++k) {
+    const int pc = cpos(hh[k].y);
+    if (pc < 0) return fail(c, MSG_ESTATE, "hole parent is not a component root");
+    hpar[hpos(hh[k].x)] = pc;
+  }
+  for (int k = 0; k < nc; ++k) cholepar[cpos(hc[k].x)] = (hc[k].y >= 0) ? hpos(hc[k].y) : -1;
+  std::vector<int> stack;
+  for (int k0 = 0; k0 < nc; ++k0) {
+    int k = k0;
+    while (cenc[k] == -2) {  // walk up the chain of enclosing holes, then unwind
+      stack.push_back(k);
+      const int h = cholepar[k];
+      if (h < 0) {
+        cenc[k] = -1;
+        stack.pop_back();
+        break;
+      }
+      k = hpar[h];
+      if ((int)stack.size() > nc) return fail(c, MSG_ESTATE, "component nesting cycle");
+    }
+    while (!stack.empty()) {
+      const int j = stack.back();
+      stack.pop_back();
+      const int h = cholepar[j];
+      cenc[j] = std::max(hidx[h].second, cenc[hpar[h]]);
+    }
+  }
+  std::vector<int> up_root(nc + nh), up_r1(nc + nh), up_r2(nc + nh);
+  for (int k = 0; k < nc; ++k) {
+    up_root[k] = cidx[k].first;
+    up_r1[k] = 1 + std::max(cidx[k].second, cenc[k]);
+    up_r2[k] = 0;
+  }
+  for (int k = 0; k < nh; ++k) {
+    up_root[nc + k] = hidx[k].first;
+    up_r1[nc + k] = 1 + std::max(hidx[k].second, cenc[hpar[k]]);
+    up_r2[nc + k] = 1 + hidx[k].second;
+  }
+  if (nc + nh) {
+    // region labels at their roots: (root, r1, r2) triples through the region-list buffer
+    int* tri = (int*)c->d_cmreg;
+    const int n3 = nc + nh;
+    HIPCHK(c, hipMemcpyAsync(tri, up_root.data(), n3 * sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(tri + n3, up_r1.data(), n3 * sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(tri + 2 * n3, up_r2.data(), n3 * sizeof(int), hipMemcpyHostToDevice, st));
+    LAUNCH(c, KID_COLOR, st, k_cm_scatter, dim3(std::max(1, (n3 + 255) / 256)), dim3(256), 0, tri, n3, R1, R2);
+  }
+  // circle((5,5), 3, 255, FILLED): half widths per |dy| from OpenCV's integer circle walk
+  int half[4] = {-1, -1, -1, -1};
+  {
+    int err = 0, dx = 3, dy = 0, plus = 1, minus = (3 << 1) - 1;
+    while (dx >= dy) {
+      half[dy] = std::max(half[dy], dx);
+      if (dx <= 3) half[dx] = std::max(half[dx], dy);
+      ++dy;
+      err += plus;
+      plus += 2;
+      const int mask = (err <= 0) - 1;
+      err -= minus & mask;
+      dx += mask;
+      minus -= mask & 2;
+    }
+  }
+  LAUNCH(c, KID_COLOR, st, k_cm_paint, rowg, dim3(256), 0, pk, L, L2, frame, R1, R2, (int32_t*)d_markers, H, W,
+         make_int4(half[0], half[1], half[2], half[3]), make_int4(0, 0, 0, 0));
+  HIPCHK(c, hipGetLastError());
+  if (c->prof) {
+    HIPCHK(c, hipStreamSynchronize(st));
+    collect_profile(c);
+  }
+  return MSG_OK;
+}
+
+int msg_color_markers(msg_ctx* c, const uint8_t* bgr, size_t bgr_stride, int rows, int cols,
+                      uint8_t* sharp, size_t sharp_stride, int32_t* markers, size_t marker_stride,
+                      int* depth) {
+  int rc = host_args(c, bgr, bgr_stride, markers, marker_stride, rows, cols);
+  if (rc) return rc;
+  const long long N = (long long)rows * cols;
+  if (N > 0 && (!sharp || sharp_stride < (size_t)cols * 3)) return fail(c, MSG_EINVAL, "bad sharp buffer");
+  HIPCHK(c, hipSetDevice(c->dev));
+  rc = ensure_stage(c, std::max(N, 1ll));
+  if (rc) return rc;
+  hipStream_t st = c->own;
+  if (N > 0)
+    HIPCHK(c, hipMemcpy2DAsync(c->d_img, (size_t)cols * 3, bgr, bgr_stride, (size_t)cols * 3, rows,
+                               hipMemcpyHostToDevice, st));
+  rc = msg_color_markers_dev(c, c->d_img, rows, cols, c->d_dst, c->d_mk, depth, st);
+  if (rc) return rc;
+  if (N > 0) {
+    HIPCHK(c, hipMemcpy2DAsync(sharp, sharp_stride, c->d_dst, (size_t)cols * 3, (size_t)cols * 3, rows,
+                               hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpy2DAsync(markers, marker_stride, c->d_mk, (size_t)cols * 4, (size_t)cols * 4,
+                               rows, hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(c, hipStreamSynchronize(st));
   return MSG_OK;
 }
 

@@ -331,6 +331,29 @@ class Segmenter:
                                                   ptr(edges), ptr(mask), self._stream(stream)))
         return depth.value, ncomp.value
 
+    def color_markers_dev(self, bgr, sharp, markers, stream=None):
+        """COLOR_METHOD marker stage (PictureService.java:301-366) on device tensors: bgr (H, W, 3)
+        uint8 in; sharp (H, W, 3) uint8 (the sharpened image the watershed floods) and markers
+        (H, W) int32 out.  Returns depth (the contour count)."""
+        H, W = bgr.shape[:2]
+        depth = ctypes.c_int(0)
+        self._check(self._L.msg_color_markers_dev(self._h, ctypes.c_void_p(bgr.data_ptr()), H, W,
+                                                  ctypes.c_void_p(sharp.data_ptr()),
+                                                  ctypes.c_void_p(markers.data_ptr()), ctypes.byref(depth),
+                                                  self._stream(stream)))
+        return depth.value
+
+    def color_markers(self, bgr):
+        """Host form: (sharp BGR uint8, markers int32, depth)."""
+        bgr, st = _img_view(bgr)
+        H, W = bgr.shape[:2]
+        sharp = np.empty((H, W, 3), np.uint8)
+        m = np.empty((H, W), np.int32)
+        depth = ctypes.c_int(0)
+        self._check(self._L.msg_color_markers(self._h, _vp(bgr), st, H, W, _vp(sharp), max(W, 1) * 3,
+                                              _vp(m), max(W, 1) * 4, ctypes.byref(depth)))
+        return sharp, m, depth.value
+
     def edge_weights_dev(self, bgr, wright, wdown, stream=None):
         H, W = bgr.shape[:2]
         self._check(self._L.msg_edge_weights_dev(self._h, ctypes.c_void_p(bgr.data_ptr()),

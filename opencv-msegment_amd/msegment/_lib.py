@@ -39,6 +39,7 @@ EXPORTS = (
     "msg_gray_hist_dev", "msg_nc_levels", "msg_nc_marker_lut", "msg_nc_markers_dev",
     "msg_nc_marker_stage_dev", "msg_nc_marker_stage",
     "msg_blur_mask_size", "msg_shape_markers_dev", "msg_shape_markers",
+    "msg_color_markers_dev", "msg_color_markers",
 )
 
 
@@ -70,7 +71,7 @@ class BrightLevel(ctypes.Structure):
     _fields_ = [("start", ctypes.c_int32), ("end", ctypes.c_int32), ("count", ctypes.c_int32)]
 
 
-NKERNELS = 20
+NKERNELS = 21
 
 
 def build(arch="gfx950"):
@@ -161,5 +162,9 @@ def load():
     L.msg_shape_markers_dev.restype = i
     L.msg_shape_markers.argtypes = [vp, vp, sz, i, i, i, vp, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
     L.msg_shape_markers.restype = i
+    L.msg_color_markers_dev.argtypes = [vp, vp, i, i, vp, vp, ctypes.POINTER(i), vp]
+    L.msg_color_markers_dev.restype = i
+    L.msg_color_markers.argtypes = [vp, vp, sz, i, i, vp, sz, vp, sz, ctypes.POINTER(i)]
+    L.msg_color_markers.restype = i
     _lib = L
     return L

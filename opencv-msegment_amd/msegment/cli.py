@@ -9,12 +9,11 @@ Reference: src/main/java/ru/shayhulud/opencvcmsegment/App.java:14-31
 
 The reference's console path keeps every step image in memory and never writes it (readPicture's
 output folder is a TODO, :129-131; only the GUI's saveResultsToFS, :194-233, writes).  ``--save``
-writes the shape method's ``result`` and ``bw_result`` the way saveResultsToFS would, into
+writes both methods' ``result`` and ``bw_result`` the way saveResultsToFS would, into
 ``outMainFolder/<name>_output/``, named by OutFileNameGenerator.generatePng
 (common/util/OutFileNameGenerator.java:14-16): ``<METHOD>_<name>_<step %05d>_<stepName>.png``.
 The step numbers are the ones the reference gives with NO_SAVE_STEPS (result 1, bw_result 2).
-
-The colour method (F2) is not built: it is reported and skipped.
+The colour method's contour numbering is unpinned against a real OpenCV build.
 
     python -m msegment.cli <picturePath> <outMainFolder> <pictureName> [--save] [--seed S]
 """
@@ -78,16 +77,26 @@ def run(argv, out=sys.stdout, service=None):
     except IOError as e:
         print("There is an error with file stream processing: %s" % e, file=out)
         return 2
-    print("colorAutoMarkerWatershed: not built (F2, DESIGN.md section 8); skipped", file=out)
     if service is None:
         from .picture_service import PictureService
 
         service = PictureService(seed=seed)
+    name = image_file_name(picture_name)
+    # App.java:28: colorAutoMarkerWatershed(args...) -- contour numbering unpinned
+    cres = service.color_auto_marker_watershed(src)
+    print("colorAutoMarkerWatershed: %dx%d, depth %d" % (src.shape[0], src.shape[1], cres.depth), file=out)
+    if save:
+        odir = os.path.join(out_main_folder, name + "_output")
+        os.makedirs(odir, exist_ok=True)
+        for step, step_name, img in ((1, "result", cres.dst), (2, "bw_result", cres.bw)):
+            path = os.path.join(odir, generate_png("COLOR_METHOD_" + name, step, step_name))
+            write_png(path, img)
+            print("wrote image %s" % path, file=out)
+    # App.java:29: shapeAutoMarkerWatershed(args...)
     res = service.shape_auto_marker_watershed(src)
     if res is None:
         print("contours is empty", file=out)  # PictureService.java:451-453
         return 0
-    name = image_file_name(picture_name)
     print("shapeAutoMarkerWatershed: %dx%d, depth %d" % (src.shape[0], src.shape[1], res.depth), file=out)
     if save:
         odir = os.path.join(out_main_folder, name + "_output")

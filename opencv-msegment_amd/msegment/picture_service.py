@@ -10,6 +10,8 @@ Reference: src/main/java/ru/shayhulud/opencvcmsegment/service/PictureService.jav
     (the caller that builds the flood's seeds from brightness levels; see not_connected_markers)
   * ``shapeAutoMarkerWatershed(ii, options)``                                :395-466
     (seeds from Canny edge rings; see shape_auto_marker_watershed)
+  * ``colorAutoMarkerWatershed(ii, options)``                                :301-392
+    (seeds from distance-transform peaks of the sharpened image; see color_auto_marker_watershed)
 
 Same names, argument meaning and error behaviour: ``watershed`` rewrites ``markers`` in place
 (like ``Imgproc.watershed``) and returns the colourised Mat; a type/size mismatch raises
@@ -22,6 +24,7 @@ from .jrandom import JavaRandom
 
 NcResult = namedtuple("NcResult", "dst bw labels levels colored_markers")
 ShapeResult = namedtuple("ShapeResult", "dst bw labels depth")
+ColorResult = namedtuple("ColorResult", "dst bw labels depth sharp")
 
 
 class PictureService:
@@ -142,3 +145,34 @@ class PictureService:
                                    torch.from_numpy(pal).to(dev) if pal is not None else None, dst, bw)
         torch.cuda.synchronize(dev)
         return ShapeResult(dst.cpu().numpy(), bw.cpu().numpy(), markers.cpu().numpy(), depth)
+
+    def color_auto_marker_watershed(self, src, options=()):
+        """PictureService.colorAutoMarkerWatershed (PictureService.java:301-392) on the GPU.
+
+        white -> black and src - 9x1 Laplacian (the sharpened image is what the watershed floods,
+        :333), Otsu bw, distanceTransform peaks, contours -> markers and depth = the contour
+        count (:355-364), then this.watershed(src, markers, depth, colored) (:378) and the
+        bw_result (:384-386).  ``options``: COLORED changes the result; the save-step options do
+        not apply here.  Returns ColorResult(dst, bw, labels = the flooded markers, depth, sharp).
+        The contour numbering is unpinned against a real OpenCV build.
+        """
+        import numpy as np
+        import torch
+
+        colored = "COLORED" in set(options)
+        src = np.ascontiguousarray(np.asarray(src, dtype=np.uint8))
+        H, W = src.shape[:2]
+        dev = torch.device("cuda", self.segmenter.device)
+        d_src = torch.from_numpy(src).to(dev)
+        sharp = torch.empty((H, W, 3), dtype=torch.uint8, device=dev)
+        markers = torch.empty((H, W), dtype=torch.int32, device=dev)
+        seg = self.segmenter
+        depth = seg.color_markers_dev(d_src, sharp, markers)
+        pal = self._palette(depth, colored)
+        dst = torch.empty((H, W, 3), dtype=torch.uint8, device=dev)
+        bw = torch.empty((H, W), dtype=torch.uint8, device=dev)
+        seg.watershed_colorize_dev(sharp, markers, markers, depth,
+                                   torch.from_numpy(pal).to(dev) if pal is not None else None, dst, bw)
+        torch.cuda.synchronize(dev)
+        return ColorResult(dst.cpu().numpy(), bw.cpu().numpy(), markers.cpu().numpy(), depth,
+                           sharp.cpu().numpy())

@@ -204,3 +204,60 @@ int oracle_bgr2gray(const uint8_t* bgr, size_t bgr_stride, int rows, int cols, u
     }
     return 0;
 }
+
+/* distanceTransform(bw, dist, DIST_L2, 5) of OpenCV 3.4.2 (imgproc/src/distransform.cpp,
+ * distanceTransform_5x5), restated for the colour-method marker stage (PictureService.java:1018-
+ * 1023, reached from :346): a two-pass raster scan of the 5x5 chamfer mask with the DIST_L2
+ * weights {1, 1.4, 2.1969} in 16-bit fixed point (65536, 91750, 143976), a border of
+ * INIT_DIST0 = INT_MAX >> 2 around the image, distances of pixels with bw == 0 are 0.
+ * Writes the raw fixed-point distances (the float image is t0 * (1.f / 65536)). */
+int oracle_chamfer5(const uint8_t* bw, int rows, int cols, uint32_t* out)
+{
+    enum { B = 2 };
+    const uint32_t HV = 65536u, DG = 91750u, LG = 143976u, INIT = 0x7fffffffu >> 2;
+    const int st = cols + 2 * B;
+    uint32_t* t = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)st * (size_t)(rows + 2 * B));
+    if (!t) return -3;
+    for (int i = 0; i < B; i++)
+        for (int j = 0; j < st; j++) {
+            t[(size_t)i * st + j] = INIT;
+            t[(size_t)(rows + 2 * B - 1 - i) * st + j] = INIT;
+        }
+    for (int i = 0; i < rows; i++) {
+        uint32_t* r = t + (size_t)(i + B) * st + B;
+        const uint8_t* s = bw + (size_t)i * cols;
+        for (int j = 0; j < B; j++) r[-j - 1] = r[cols + j] = INIT;
+        for (int j = 0; j < cols; j++) {
+            if (!s[j]) { r[j] = 0; continue; }
+            uint32_t t0 = r[j - 2 * st - 1] + LG, v;
+            v = r[j - 2 * st + 1] + LG; if (t0 > v) t0 = v;
+            v = r[j - st - 2] + LG; if (t0 > v) t0 = v;
+            v = r[j - st - 1] + DG; if (t0 > v) t0 = v;
+            v = r[j - st] + HV; if (t0 > v) t0 = v;
+            v = r[j - st + 1] + DG; if (t0 > v) t0 = v;
+            v = r[j - st + 2] + LG; if (t0 > v) t0 = v;
+            v = r[j - 1] + HV; if (t0 > v) t0 = v;
+            r[j] = t0;
+        }
+    }
+    for (int i = rows - 1; i >= 0; i--) {
+        uint32_t* r = t + (size_t)(i + B) * st + B;
+        for (int j = cols - 1; j >= 0; j--) {
+            uint32_t t0 = r[j], v;
+            if (t0 > HV) {
+                v = r[j + 2 * st + 1] + LG; if (t0 > v) t0 = v;
+                v = r[j + 2 * st - 1] + LG; if (t0 > v) t0 = v;
+                v = r[j + st + 2] + LG; if (t0 > v) t0 = v;
+                v = r[j + st + 1] + DG; if (t0 > v) t0 = v;
+                v = r[j + st] + HV; if (t0 > v) t0 = v;
+                v = r[j + st - 1] + DG; if (t0 > v) t0 = v;
+                v = r[j + st - 2] + LG; if (t0 > v) t0 = v;
+                v = r[j + 1] + HV; if (t0 > v) t0 = v;
+                r[j] = t0;
+            }
+            out[(size_t)i * cols + j] = t0;
+        }
+    }
+    free(t);
+    return 0;
+}

@@ -36,6 +36,8 @@ def lib():
         L.oracle_colorize.restype = ctypes.c_int
         L.oracle_bgr2gray.argtypes = [u8p, sz, ctypes.c_int, ctypes.c_int, u8p, sz]
         L.oracle_bgr2gray.restype = ctypes.c_int
+        L.oracle_chamfer5.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
+        L.oracle_chamfer5.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -78,4 +80,16 @@ def bgr2gray(bgr):
     H, W, _ = bgr.shape
     out = np.empty((H, W), dtype=np.uint8)
     lib().oracle_bgr2gray(_p(bgr, ctypes.c_uint8), W * 3, H, W, _p(out, ctypes.c_uint8), W)
+    return out
+
+
+def chamfer5(bw):
+    """OpenCV 3.4.2 distanceTransform(DIST_L2, 5) raw fixed-point distances (uint32, x 2^-16)."""
+    bw = np.ascontiguousarray(bw, dtype=np.uint8)
+    H, W = bw.shape
+    out = np.zeros((H, W), np.uint32)
+    if H and W:
+        rc = lib().oracle_chamfer5(_p(bw, ctypes.c_uint8), H, W, _p(out, ctypes.c_uint32))
+        if rc:
+            raise MemoryError("oracle_chamfer5: %d" % rc)
     return out

@@ -1,6 +1,6 @@
 """The console entry point (msegment.cli) against App.java:14-31 and the reference's output naming
 (OutFileNameGenerator.java:14-16).  CPU tests drive it with a stand-in service (argument handling,
-echo, naming, the null-contour branch); the GPU test runs the real shape pipeline through it and
+echo, naming, the null-contour branch); the GPU test runs the real colour and shape pipelines through it and
 compares the written PNGs with a direct PictureService call on the same picture."""
 import io
 import os
@@ -9,13 +9,22 @@ import numpy as np
 import pytest
 
 from msegment import cli
-from msegment.picture_service import ShapeResult
+from msegment.picture_service import ColorResult, ShapeResult
 
 
 class _FakeService:
-    def __init__(self, res):
+    def __init__(self, res, cres=None):
         self.res = res
+        self.cres = cres
         self.seen = None
+
+    def color_auto_marker_watershed(self, src):
+        self.seen = src
+        if self.cres is not None:
+            return self.cres
+        h, w = src.shape[:2]
+        z = np.zeros((h, w, 3), np.uint8)
+        return ColorResult(z, z[:, :, 0], np.zeros((h, w), np.int32), 0, z)
 
     def shape_auto_marker_watershed(self, src):
         self.seen = src
@@ -55,20 +64,29 @@ def test_reads_bgr_and_saves_named_outputs(tmp_path):
     h, w = bgr.shape[:2]
     dst = np.full((h, w, 3), 7, np.uint8)
     bw = np.full((h, w), 9, np.uint8)
-    svc = _FakeService(ShapeResult(dst, bw, np.zeros((h, w), np.int32), 3))
+    cdst = np.full((h, w, 3), 5, np.uint8)
+    cbw = np.full((h, w), 6, np.uint8)
+    svc = _FakeService(ShapeResult(dst, bw, np.zeros((h, w), np.int32), 3),
+                       ColorResult(cdst, cbw, np.zeros((h, w), np.int32), 11, cdst))
     out = io.StringIO()
     rc = cli.run([str(tmp_path), str(tmp_path), "pic.test.png", "--save"], out=out, service=svc)
     assert rc == 0
     assert np.array_equal(svc.seen, bgr)          # imread order: BGR
     odir = os.path.join(str(tmp_path), "pic_output")
     names = sorted(os.listdir(odir))
-    assert names == ["SHAPE_METHOD_pic_00001_result.png", "SHAPE_METHOD_pic_00002_bw_result.png"]
+    assert names == ["COLOR_METHOD_pic_00001_result.png", "COLOR_METHOD_pic_00002_bw_result.png",
+                     "SHAPE_METHOD_pic_00001_result.png", "SHAPE_METHOD_pic_00002_bw_result.png"]
     from PIL import Image
 
-    got = np.asarray(Image.open(os.path.join(odir, names[0])).convert("RGB"))[:, :, ::-1]
+    got = np.asarray(Image.open(os.path.join(odir, names[2])).convert("RGB"))[:, :, ::-1]
     assert np.array_equal(got, dst)
-    assert np.array_equal(np.asarray(Image.open(os.path.join(odir, names[1]))), bw)
-    assert "depth 3" in out.getvalue()
+    assert np.array_equal(np.asarray(Image.open(os.path.join(odir, names[3]))), bw)
+    got = np.asarray(Image.open(os.path.join(odir, names[0])).convert("RGB"))[:, :, ::-1]
+    assert np.array_equal(got, cdst)
+    assert np.array_equal(np.asarray(Image.open(os.path.join(odir, names[1]))), cbw)
+    text = out.getvalue()
+    assert "colorAutoMarkerWatershed: 24x40, depth 11" in text and "depth 3" in text
+    assert text.index("colorAutoMarkerWatershed") < text.index("shapeAutoMarkerWatershed")  # App.java:28-29
 
 
 def test_no_contours_returns_quietly(tmp_path):
@@ -77,7 +95,8 @@ def test_no_contours_returns_quietly(tmp_path):
     rc = cli.run([str(tmp_path), str(tmp_path), "pic.test.png", "--save"], out=out,
                  service=_FakeService(None))
     assert rc == 0 and "contours is empty" in out.getvalue()
-    assert not os.path.exists(os.path.join(str(tmp_path), "pic_output"))
+    odir = os.path.join(str(tmp_path), "pic_output")
+    assert sorted(os.listdir(odir)) == ["COLOR_METHOD_pic_00001_result.png", "COLOR_METHOD_pic_00002_bw_result.png"]
 
 
 @pytest.mark.gpu
@@ -101,3 +120,8 @@ def test_cli_shape_pipeline_matches_service(tmp_path):
     assert np.array_equal(got[:, :, ::-1], ref.dst)
     got_bw = np.asarray(Image.open(os.path.join(odir, "SHAPE_METHOD_m_00002_bw_result.png")))
     assert np.array_equal(got_bw, ref.bw)
+    cref = PictureService(seed=4).color_auto_marker_watershed(img)
+    got = np.asarray(Image.open(os.path.join(odir, "COLOR_METHOD_m_00001_result.png")).convert("RGB"))
+    assert np.array_equal(got[:, :, ::-1], cref.dst)
+    got_bw = np.asarray(Image.open(os.path.join(odir, "COLOR_METHOD_m_00002_bw_result.png")))
+    assert np.array_equal(got_bw, cref.bw)
