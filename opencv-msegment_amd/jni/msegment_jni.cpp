@@ -5,7 +5,7 @@
 // Replaces the OpenCV 3.4.2 JNI entry Java_org_opencv_imgproc_Imgproc_watershed_10 reached from
 // PictureService.java:909, plus the per-pixel colorByIndexes loop (PictureService.java:913-936),
 // and the marker stages of notConnectedMarkers (PictureService.java:476-828) and
-// shapeAutoMarkerWatershed (PictureService.java:402-452).
+// shapeAutoMarkerWatershed (PictureService.java:402-452) and colorAutoMarkerWatershed (:301-366).
 //
 // Every Java array is checked against the sizes rows/cols/depth imply before anything is read
 // (a short array returns MSG_EINVAL instead of letting libmsegment run past it), and the arrays
@@ -137,6 +137,30 @@ JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNativ
   const int rc = msg_shape_markers(c, reinterpret_cast<const uint8_t*>(b.data()), (size_t)cols * 3, rows, cols,
                                    0, reinterpret_cast<int32_t*>(m.data()), (size_t)cols * 4, &depth, &ncomp);
   if (rc) return rc;
+  env->SetIntArrayRegion(markers, 0, (jsize)n, m.data());
+  return depth;
+}
+
+// colorAutoMarkerWatershed's marker stage (PictureService.java:301-366): the sharpened image (the
+// src the reference then floods, :333) and the markers out, returns the contour count (the
+// watershed depth) or a negative MSG_E* code.
+JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_colorMarkers(
+    JNIEnv* env, jclass, jlong ctx, jbyteArray bgr, jint rows, jint cols, jbyteArray sharp, jintArray markers) {
+  msg_ctx* c = reinterpret_cast<msg_ctx*>(ctx);
+  if (!c || !fits(env, bgr, rows, cols, 3) || !fits(env, sharp, rows, cols, 3) || !fits(env, markers, rows, cols, 1))
+    return MSG_EINVAL;
+  const long long n = (long long)rows * cols;
+  std::vector<jbyte> b, sh;
+  std::vector<jint> m;
+  if (!alloc(b, 3 * n) || !alloc(sh, 3 * n) || !alloc(m, n)) return MSG_ENOMEM;
+  env->GetByteArrayRegion(bgr, 0, (jsize)(3 * n), b.data());
+  if (env->ExceptionCheck()) return MSG_EINVAL;
+  int depth = 0;
+  const int rc = msg_color_markers(c, reinterpret_cast<const uint8_t*>(b.data()), (size_t)cols * 3, rows, cols,
+                                   reinterpret_cast<uint8_t*>(sh.data()), (size_t)cols * 3,
+                                   reinterpret_cast<int32_t*>(m.data()), (size_t)cols * 4, &depth);
+  if (rc) return rc;
+  env->SetByteArrayRegion(sharp, 0, (jsize)(3 * n), sh.data());
   env->SetIntArrayRegion(markers, 0, (jsize)n, m.data());
   return depth;
 }

@@ -96,6 +96,38 @@ public final class MSegmentNative {
         return markers;
     }
 
+    /** Returns the contour count (>= 0) or a negative MSG_E* code; sharp and markers filled. */
+    private static native int colorMarkers(long ctx, byte[] bgr, int rows, int cols, byte[] sharp, int[] markers);
+
+    /**
+     * Drop-in for the marker stage of PictureService.colorAutoMarkerWatershed
+     * (PictureService.java:301-366): returns the markers (CV_32SC1), writes the sharpened image
+     * the reference then floods (:333) into sharpOut (CV_8UC3, allocated here) and the contour
+     * count (the depth passed to watershed) into depthOut[0].
+     */
+    public static Mat colorMarkers(Mat src, Mat sharpOut, int[] depthOut) {
+        if (src.type() != CvType.CV_8UC3) {
+            throw new CvException("colorMarkers: src must be CV_8UC3");
+        }
+        int rows = src.rows();
+        int cols = src.cols();
+        byte[] bgr = new byte[rows * cols * 3];
+        byte[] sh = new byte[rows * cols * 3];
+        int[] mk = new int[rows * cols];
+        src.get(0, 0, bgr);
+        long ctx = CTX.get();
+        int d = colorMarkers(ctx, bgr, rows, cols, sh, mk);
+        if (d < 0) {
+            throw new CvException("libmsegment error " + d + ": " + lastError(ctx));
+        }
+        depthOut[0] = d;
+        sharpOut.create(src.size(), CvType.CV_8UC3);
+        sharpOut.put(0, 0, sh);
+        Mat markers = new Mat(src.size(), CvType.CV_32SC1);
+        markers.put(0, 0, mk);
+        return markers;
+    }
+
     /** Drop-in for PictureService.watershed(src, markers, depth, colored) given its palette. */
     public static Mat watershed(Mat src, Mat markers, int depth, byte[] paletteOrNull) {
         if (src.type() != CvType.CV_8UC3 || markers.type() != CvType.CV_32SC1

@@ -22,6 +22,8 @@ jint Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_ncMarkers(JNIEnv
                                                                           jintArray);
 jint Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_shapeMarkers(JNIEnv*, jclass, jlong,
                                                                              jbyteArray, jint, jint, jintArray);
+jint Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_colorMarkers(JNIEnv*, jclass, jlong, jbyteArray,
+                                                                             jint, jint, jbyteArray, jintArray);
 }
 
 struct Bytes : _jbyteArray {
@@ -117,6 +119,10 @@ static int validate() {
              &env, nullptr, fake, bytes(3 * N - 2), R, C, ints(N)), "shape short bgr");
   expect(Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_shapeMarkers(
              &env, nullptr, fake, bytes(3 * N), R, C, nullptr), "shape null markers");
+  expect(Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_colorMarkers(
+             &env, nullptr, fake, bytes(3 * N), R, C, bytes(3 * N - 1), ints(N)), "color short sharp");
+  expect(Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_colorMarkers(
+             &env, nullptr, fake, bytes(3 * N), R, C, bytes(3 * N), ints(N - 1)), "color short markers");
   if (g_critical) {
     std::printf("FAIL critical regions taken: %d\n", g_critical);
     ++bad;
