@@ -8,7 +8,7 @@
 //   findContours(RETR_CCOMP) + drawContours + circle             :356-364   CCL (shape_kernels.hip),
 //                                                                           k_cm_regions, host order, k_cm_paint
 //
-// Exact restatements (oracle/color_oracle.py, oracle/ws_oracle.c: oracle_chamfer5): the sharpen is
+// Exact restatements (the CPU checker lives under oracle/, test-only): the sharpen is
 // integer arithmetic; the chamfer distance is the min-plus closure of the 5x5 mask, which the
 // two-pass raster scan of OpenCV computes and which in-place relaxation sweeps reach as well
 // (values only decrease and every value is a path length); normalisation and the 0.4 threshold
