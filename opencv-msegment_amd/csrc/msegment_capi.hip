@@ -455,11 +455,11 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
     prev_end = it - 1;
   }
   {
-    const long long nunits = (long long)((H + 3) / 4) * ws.Wt * 8;
-    const int grid = (int)std::min<long long>((nunits + 255) / 256, 8192);
+    const long long nrows = (long long)((H + 3) / 4) * ws.Wt * 4;  // one tile row per lane
+    const int grid = (int)std::min<long long>((nrows + 255) / 256, 1 << 20);
     const size_t shm = (d_dst && d_pal && depth <= PAL_LDS_MAX) ? (size_t)std::max(depth, 1) * 4 : 0;
     LAUNCH(c, KID_UNTILE, st, k_untile, dim3(grid), dim3(256), shm, c->d_px, H, W, ws.Wt, d_labels,
-           depth, d_pal, d_dst, d_gray);
+           depth, d_pal, d_dst, d_gray, &c->d_ctl->error);
     HIPCHK(c, hipGetLastError());
   }
   Ctl tail;
@@ -486,6 +486,23 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   if (tail.error & ERR_TIMEOUT)
     return fail(c, MSG_ETIMEOUT, "in-kernel wait timed out (grid not co-resident?)");
   if (tail.error & ERR_CAPACITY) return fail(c, MSG_ESTATE, "bucket capacity exceeded");
+  if (tail.error & ERR_REPUSH)
+    return fail(c, MSG_ESTATE, "a push found its target already queued or labelled (%llu pushes, first at site %llu: "
+                "labelled %llu, queued %llu; last prev %d dest %u, epoch %u rank %u; flood epochs %u..)", dgv[7], dgv[11], dgv[12], dgv[13],
+                (int)(dgv[14] >> 32), (unsigned)dgv[14], (unsigned)(dgv[15] >> 32), (unsigned)dgv[15],
+                c->epoch - (unsigned)std::min<long long>(tail.batches + 4, 0x7fffffff));
+  if (tail.error & ERR_LEFTOVER) {
+    unsigned long long lo[8] = {0};
+    if (c->diag) {  // classify them (k_leftover_diag) for the message
+      HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 8 * sizeof(unsigned long long), st));
+      const long long nt = (long long)((H + 3) / 4) * ws.Wt * 16;
+      LAUNCH(c, KID_UNTILE, st, k_leftover_diag, dim3(1024), dim3(256), 0, ws, nt, c->d_diag);
+      HIPCHK(c, hipMemcpyAsync(lo, c->d_diag, sizeof(lo), hipMemcpyDeviceToHost, st));
+      HIPCHK(c, hipStreamSynchronize(st));
+    }
+    return fail(c, MSG_ESTATE, "queued pixels left at the end of the flood (%llu: phase-1 %llu, popped %llu, "
+                "slot reused %llu; last tiled %llu slot %llu)", lo[3], lo[0], lo[1], lo[2], lo[4], lo[5]);
+  }
   if (tail.error) return fail(c, MSG_ESTATE, "device consistency check failed (%d)", tail.error);
   if (!tail.done) return fail(c, MSG_ESTATE, "flood did not finish");
   return MSG_OK;
@@ -559,6 +576,10 @@ int run_batch(msg_ctx* c, int n, F fn) {
   for (int w = 0; w < k; ++w) {
     c->subs[w]->res_grid = c->res_grid;
     c->subs[w]->spec = c->spec;
+    if (c->subs[w]->diag != c->diag || c->subs[w]->inject != c->inject) {
+      rc = msg_set_diag(c->subs[w], c->inject ? 2 : c->diag ? 1 : 0);
+      if (rc) return rc;
+    }
   }
   std::vector<int> rcs(k, MSG_OK);
   std::vector<msg_stats> st(k);
@@ -934,13 +955,15 @@ int msg_edge_weights_dev(msg_ctx* c, const void* d_bgr, void* d_wright, void* d_
   hipStream_t st = scope.st;
   const bool vec = cols % 16 == 0 && (((uintptr_t)d_bgr | (uintptr_t)d_wright | (uintptr_t)d_wdown) & 15) == 0;
   if (vec) {
-    if (N <= (8ll << 20) * 4) {  // up to 2 x 4096^2 pixels: 2 rows per thread (ws_kernels.hip)
-      const long long th = (long long)((rows + 1) / 2) * (cols / 16);
-      LAUNCH(c, KID_EDGE, st, k_edge_weights16<2>, dim3((unsigned)((th + 255) / 256)), dim3(256), 0,
+    // rows per thread measured per size (scripts/exp/stream_variants.hip): 1 up to 4096^2
+    // (14.3 us vs 15.7 for 2), 2 above (8192^2: 61.4 us vs 63.0 for 4 and 64.9 for 1)
+    if (N <= (1ll << 24)) {
+      const long long th = (long long)rows * (cols / 16);
+      LAUNCH(c, KID_EDGE, st, k_edge_weights16<1>, dim3((unsigned)((th + 255) / 256)), dim3(256), 0,
              (const uint8_t*)d_bgr, (uint8_t*)d_wright, (uint8_t*)d_wdown, rows, cols);
     } else {
-      const long long th = (long long)((rows + 3) / 4) * (cols / 16);
-      LAUNCH(c, KID_EDGE, st, k_edge_weights16<4>, dim3((unsigned)((th + 255) / 256)), dim3(256), 0,
+      const long long th = (long long)((rows + 1) / 2) * (cols / 16);
+      LAUNCH(c, KID_EDGE, st, k_edge_weights16<2>, dim3((unsigned)((th + 255) / 256)), dim3(256), 0,
              (const uint8_t*)d_bgr, (uint8_t*)d_wright, (uint8_t*)d_wdown, rows, cols);
     }
   } else {

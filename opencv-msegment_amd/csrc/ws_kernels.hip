@@ -68,21 +68,23 @@ __device__ __forceinline__ void st_granule(unsigned long long* p, unsigned long 
 // the next strip's first), one dword per row for the right neighbour of pixel 15, one 16-B store
 // per output row.  Blocks are renumbered XCD-aware (blocks b, b + 8, ... run on one XCD under
 // round-robin placement and get consecutive strips), so the extra row is mostly the one that
-// XCD's L2 just fetched for its neighbour strip: R = 2 is fastest at 4096^2 (20.6 vs 22.6 us for
-// R = 4 without the renumbering), R = 4 at 8192^2 and above (scripts/exp/stencil_variants.hip;
-// staging the rows through LDS for fully contiguous wave loads measured 10-20% slower).
+// XCD's L2 just fetched for its neighbour strip.  The kernel is VALU-heavy for its bytes (6
+// channel differences and 2 maxima per pixel), so every channel byte is extracted once per row
+// and each |a - b| is one v_sad_u16 (operands < 2^16): 16.5 -> ~10 VALU ops per pixel, which
+// took the 4096^2 launch from 18.1 to 14.7 us (R = 1; scripts/exp/stream_variants.hip).  Frames
+// are <= 2^28 pixels (check_size), so 32-bit offsets suffice.
 // k_edge_weights: any shape, 4 pixels per thread.
-__device__ __forceinline__ uint32_t byte_of(const uint32_t* w, int i) { return (w[i >> 2] >> (8 * (i & 3))) & 255u; }
-__device__ __forceinline__ uint32_t linf3(const uint32_t* wa, int ia, const uint32_t* wb, int ib) {
-  uint32_t m = 0;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int x = (int)byte_of(wa, ia + k), y = (int)byte_of(wb, ib + k);
-    m = max(m, (uint32_t)abs(x - y));
-  }
-  return m;
+__device__ __forceinline__ uint32_t absdiff(uint32_t x, uint32_t y) { return __builtin_amdgcn_sad_u16(x, y, 0u); }
+__device__ __forceinline__ uint32_t linf_ch(const uint32_t* p, const uint32_t* q) {
+  return max(max(absdiff(p[0], q[0]), absdiff(p[1], q[1])), absdiff(p[2], q[2]));
 }
-
+// the 17 pixels (16 + the right neighbour) of a row segment as channel values
+__device__ __forceinline__ void unpack17(const uint32_t* w, uint32_t px[17][3]) {
+#pragma unroll
+  for (int k = 0; k < 17; ++k)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) px[k][c] = (w[(3 * k + c) >> 2] >> (8 * ((3 * k + c) & 3))) & 255u;
+}
 
 __device__ __forceinline__ void ld48(const uint8_t* p, uint32_t* w) {
   const uint4* a = reinterpret_cast<const uint4*>(p);
@@ -96,43 +98,52 @@ template <int EW_ROWS>
 __global__ __launch_bounds__(256) void k_edge_weights16(const uint8_t* __restrict__ img,
                                                         uint8_t* __restrict__ wr,
                                                         uint8_t* __restrict__ wd, int H, int W) {
-  const int segs = W >> 4;
+  const unsigned segs = (unsigned)W >> 4;
   unsigned b = blockIdx.x;
   const unsigned per_xcd = gridDim.x / 8;
   if (b < per_xcd * 8) b = (b % 8) * per_xcd + b / 8;  // a bijection on the first 8*per_xcd blocks
-  const long long t = (long long)b * blockDim.x + threadIdx.x;
-  const int strips = (H + EW_ROWS - 1) / EW_ROWS;
-  if (t >= (long long)strips * segs) return;
-  const int st = (int)(t / segs), sx = (int)(t - (long long)st * segs);
-  const int r0 = st * EW_ROWS;
+  const unsigned t = b * blockDim.x + threadIdx.x;
+  const unsigned strips = ((unsigned)H + EW_ROWS - 1) / EW_ROWS;
+  if (t >= strips * segs) return;
+  const unsigned st = t / segs, sx = t - st * segs;
+  const int r0 = (int)st * EW_ROWS;
   const bool has_r = sx + 1 < segs;
   // every load of the strip first: EW_ROWS + 1 rows of 48 B, the right neighbours' first dwords
   uint32_t rows[EW_ROWS + 1][13];
 #pragma unroll
   for (int i = 0; i <= EW_ROWS; ++i) {
     const int r = r0 + i;
-    const long long p0 = (long long)r * W + 16ll * sx;
+    const unsigned p0 = (unsigned)r * (unsigned)W + 16u * sx;
+#pragma unroll
+    for (int k = 0; k < 13; ++k) rows[i][k] = 0;
     if (r < H) {
-      ld48(img + 3 * p0, rows[i]);
-      rows[i][12] = (has_r && i < EW_ROWS) ? *reinterpret_cast<const uint32_t*>(img + 3 * (p0 + 16)) : 0u;
+      ld48(img + 3u * p0, rows[i]);
+      if (has_r && i < EW_ROWS) rows[i][12] = *reinterpret_cast<const uint32_t*>(img + 3u * (p0 + 16u));
     }
   }
+  uint32_t cur[17][3], nxt[17][3];
+  unpack17(rows[0], cur);
 #pragma unroll
   for (int i = 0; i < EW_ROWS; ++i) {
     const int r = r0 + i;
     if (r >= H) break;
     const bool has_d = r + 1 < H;
+    unpack17(rows[i + 1], nxt);
     uint32_t orr[4] = {0, 0, 0, 0}, odd[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      const uint32_t vr = (k < 15 || has_r) ? linf3(rows[i], 3 * k, rows[i], 3 * k + 3) : 0u;
-      const uint32_t vd = has_d ? linf3(rows[i], 3 * k, rows[i + 1], 3 * k) : 0u;
+      const uint32_t vr = (k < 15 || has_r) ? linf_ch(cur[k], cur[k + 1]) : 0u;
+      const uint32_t vd = has_d ? linf_ch(cur[k], nxt[k]) : 0u;
       orr[k >> 2] |= vr << (8 * (k & 3));
       odd[k >> 2] |= vd << (8 * (k & 3));
     }
-    const long long p0 = (long long)r * W + 16ll * sx;
+    const unsigned p0 = (unsigned)r * (unsigned)W + 16u * sx;
     *reinterpret_cast<uint4*>(wr + p0) = make_uint4(orr[0], orr[1], orr[2], orr[3]);
     *reinterpret_cast<uint4*>(wd + p0) = make_uint4(odd[0], odd[1], odd[2], odd[3]);
+#pragma unroll
+    for (int k = 0; k < 17; ++k)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) cur[k][c] = nxt[k][c];
   }
 }
 
@@ -709,6 +720,26 @@ __global__ __launch_bounds__(256) void k_compact(Ws ws, int nrc) {
 }
 
 __device__ __forceinline__ int ld_state(const Ws& ws, long long t) { return ws.mk[t]; }
+// Wait until this wave's global stores have completed.  __syncthreads() orders LDS but, as
+// compiled for gfx950 (s_waitcnt lgkmcnt(0); s_barrier), not one wave's global stores before
+// another wave's later global loads: with 8 concurrent floods (scripts/stress_inflight_dev.py,
+// GPU_MAX_HW_QUEUES=16) a small-batch loop's next gather in another wave read a pushed pixel as
+// still unknown and queued it twice.  Used before every barrier that hands global state
+// written by some waves to loads by others within one workgroup.
+__device__ __forceinline__ void stores_done() { __builtin_amdgcn_s_waitcnt(0); }
+
+// Diagnostics (msg_set_diag): a push target must still be unknown (0).  Counts violations by kind
+// and records the first push site that saw one (1 k_scatter, 2 small-batch loop, 3 tiny loop).
+__device__ __noinline__ void check_push(const Ws& ws, long long n, int dest, unsigned epoch, int rank, int site) {
+  const int prev = __hip_atomic_load(ws.mk + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (prev == 0) return;
+  atomicOr(&ws.ctl->error, ERR_REPUSH);
+  atomicAdd(&ws.diag[7], 1ull);
+  atomicAdd(&ws.diag[prev <= -3 ? 13 : 12], 1ull);
+  atomicCAS(&ws.diag[11], 0ull, (unsigned long long)site);
+  ws.diag[14] = ((unsigned long long)(uint32_t)prev << 32) | (uint32_t)dest;
+  ws.diag[15] = ((unsigned long long)epoch << 32) | (uint32_t)rank;
+}
 // 32-bit form of nb_of for indices taken from the margin start (a multiple of 16: tile-aligned)
 __device__ __forceinline__ int nbi(int t, int d, int Wt) {
   const int row = Wt << 4;
@@ -1402,9 +1433,13 @@ __device__ void scatter_chunks(const Ws& ws, const Batch& B, int first, int stri
         continue;
       }
       const long long n = (B.mode == 0) ? nb_of(p, d, Wt) : p;
+      if (ws.diag && B.mode == 0) check_push(ws, n, dest, B.epoch, i0 + tid, 1);
       st_state(ws, n, queued_state(dest));
       ws.qbuf[dest] = (int32_t)n;
     }
+    // the block's own later reads of these states (k_scan's small-batch loop after it) come from
+    // other waves: a barrier alone does not order one wave's stores before another's loads
+    stores_done();
     __syncthreads();  // before the next sub-round reuses run/wcnt
   }
 }
@@ -1579,6 +1614,7 @@ __device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qba
         continue;
       }
       const long long n = nb_of(it.p, d, Wt);
+      if (ws.diag) check_push(ws, n, dest, B.epoch, i, 3);
       st_state(ws, n, queued_state(dest));
       ws.qbuf[dest] = (int32_t)n;
       ++pushed;
@@ -1954,10 +1990,12 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
           continue;
         }
         const long long n = nb_of(p, d, Wt);
+        if (ws.diag) check_push(ws, n, dest, B.epoch, i, 2);
         st_state(ws, n, queued_state(dest));
         ws.qbuf[dest] = (int32_t)n;
         ++pushed;
       }
+      stores_done();  // the next batch's gathers run in other waves (see stores_done)
       __syncthreads();
       if (tid < NQ) {
         s_tail[tid] += s_tot[tid];
@@ -2108,6 +2146,30 @@ __global__ __launch_bounds__(256) void k_colorize(const int32_t* __restrict__ la
   }
 }
 
+// Diagnostics for ERR_LEFTOVER (msg_set_diag on): classify the queued states left after a flood.
+// out[0] phase-1 states, out[1] queued states whose slot lies below its bucket's head (popped, so
+// the label write was lost), out[2] queued states whose slot holds another pixel (the push was
+// overwritten), out[3] all leftovers, out[4] / out[5] the last one's tiled index and slot.
+__global__ __launch_bounds__(256) void k_leftover_diag(Ws ws, long long nt, unsigned long long* out) {
+  const Ctl* ctl = ws.ctl;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += (long long)gridDim.x * blockDim.x) {
+    const int s = ws.mk[t];
+    if (s > -3) continue;
+    atomicAdd(out + 3, 1ull);
+    if (s < -3 - (1 << 29)) {
+      atomicAdd(out + 0, 1ull);
+      continue;
+    }
+    const int slot = -3 - s;
+    int lv = 0;
+    while (lv + 1 < NQ && ctl->qbase[lv + 1] <= slot) ++lv;
+    if (slot < ctl->qbase[lv] + ctl->qhead[lv]) atomicAdd(out + 1, 1ull);
+    if ((long long)slot < ws.qcap && ws.qbuf[slot] != (int32_t)t) atomicAdd(out + 2, 1ull);
+    out[4] = (unsigned long long)t;
+    out[5] = (unsigned long long)slot;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // End of the flood: tiled states -> the caller's row-major label map (cv::watershed's in-place
 // markers), fused with colorByIndexes (PictureService.java:913-936) + optional BGR2GRAY when dst
@@ -2124,9 +2186,13 @@ __device__ __forceinline__ uint32_t label_colour(int x, int depth, const uint8_t
 __global__ __launch_bounds__(256) void k_untile(const int32_t* __restrict__ mk, int H, int W, int Wt,
                                                 int32_t* __restrict__ lab, int depth,
                                                 const uint8_t* __restrict__ pal,
-                                                uint8_t* __restrict__ dst, uint8_t* __restrict__ gray) {
-  // lane = one 8-B unit of two states = 2 pixels of a tile row: loads are lane-contiguous, and
-  // the 16 lanes of one tile row of 8 consecutive tiles store 128 B of labels
+                                                uint8_t* __restrict__ dst, uint8_t* __restrict__ gray,
+                                                int* __restrict__ err) {
+  // lane = one tile row (16 B of states = 4 pixels): loads are lane-contiguous (a wave reads 16
+  // whole tiles), and the 16 lanes of one tile row of a wave store 256 B of labels, 192 B of
+  // colours and 64 B of gray, each one 16-B / 12-B / 4-B store per lane (the 8-B unit layout it
+  // replaces stored colours as three 2-B pieces: 33.5 -> 28.3 us at 4096^2 in
+  // scripts/exp/stream_variants.hip).  Frames are <= 2^28 pixels: 32-bit tile arithmetic.
   extern __shared__ __attribute__((aligned(16))) uint32_t spal[];
   const bool lds_pal = dst != nullptr && pal != nullptr && depth <= PAL_LDS_MAX;
   if (lds_pal) {
@@ -2134,49 +2200,53 @@ __global__ __launch_bounds__(256) void k_untile(const int32_t* __restrict__ mk, 
       spal[k] = (uint32_t)pal[3 * k] | ((uint32_t)pal[3 * k + 1] << 8) | ((uint32_t)pal[3 * k + 2] << 16);
     __syncthreads();
   }
-  const long long nunits = (long long)((H + 3) >> 2) * Wt * 8;
-  const bool even = (W & 1) == 0;
-  const bool v2 = even && (((uintptr_t)lab) & 7) == 0;
-  const bool v3 = even && dst != nullptr && (((uintptr_t)dst) & 1) == 0;
-  const bool vg = even && gray != nullptr && (((uintptr_t)gray) & 1) == 0;
-  for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < nunits;
-       u += (long long)gridDim.x * blockDim.x) {
-    const long long tt = u >> 3;
-    const int k = (int)(u & 7);
-    const int r = (int)(tt / Wt) * 4 + (k >> 1), c = (int)(tt % Wt) * 4 + 2 * (k & 1);
-    if (r >= H || c >= W) continue;
-    const int2 a = reinterpret_cast<const int2*>(mk)[u];
-    const int l[2] = {a.x, a.y};
-    const long long q = (long long)r * W + c;
-    const bool both = c + 1 < W;
-    if (both && v2) *reinterpret_cast<int2*>(lab + q) = make_int2(l[0], l[1]);
-    else for (int j = 0; j < 2 && c + j < W; ++j) lab[q + j] = l[j];
+  const unsigned nrows = (unsigned)((H + 3) >> 2) * (unsigned)Wt * 4u;
+  const bool w4 = (W & 3) == 0;
+  const bool v4 = w4 && (((uintptr_t)lab) & 15) == 0;
+  const bool v3 = w4 && dst != nullptr && (((uintptr_t)dst) & 3) == 0;
+  const bool vg = w4 && gray != nullptr && (((uintptr_t)gray) & 3) == 0;
+  for (unsigned u = blockIdx.x * blockDim.x + threadIdx.x; u < nrows; u += gridDim.x * blockDim.x) {
+    const unsigned tt = u >> 2, ty = tt / (unsigned)Wt;
+    const int r = (int)(ty * 4u + (u & 3u)), c = (int)((tt - ty * (unsigned)Wt) * 4u);
+    if (r >= H) continue;
+    const int4 s = reinterpret_cast<const int4*>(mk)[u];
+    const int l[4] = {s.x, s.y, s.z, s.w};
+    const unsigned q = (unsigned)r * (unsigned)W + (unsigned)c;
+    const int cnt = min(4, W - c);
+    // consistency: the flood pops everything it queues, so no queued or phase-1 state (<= -3) is
+    // left (a lost push or label write would otherwise end as a silently wrong label)
+    bool left = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) left |= j < cnt && l[j] <= -3;
+    if (left) atomicOr(err, ERR_LEFTOVER);
+    if (cnt == 4 && v4) *reinterpret_cast<int4*>(lab + q) = s;
+    else for (int j = 0; j < cnt; ++j) lab[q + j] = l[j];
     if (dst == nullptr) continue;
-    const uint32_t c0 = label_colour(l[0], depth, pal, lds_pal, spal);
-    const uint32_t c1 = label_colour(l[1], depth, pal, lds_pal, spal);
-    uint8_t* o = dst + q * 3;
-    if (both && v3) {  // B0G0 R0B1 G1R1
-      reinterpret_cast<uint16_t*>(o)[0] = (uint16_t)(c0 & 0xffffu);
-      reinterpret_cast<uint16_t*>(o)[1] = (uint16_t)(((c0 >> 16) & 0xffu) | ((c1 & 0xffu) << 8));
-      reinterpret_cast<uint16_t*>(o)[2] = (uint16_t)((c1 >> 8) & 0xffffu);
+    uint32_t col[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) col[j] = label_colour(l[j], depth, pal, lds_pal, spal);
+    uint8_t* o = dst + 3u * q;
+    if (cnt == 4 && v3) {  // B0G0R0B1 G1R1B2G2 R2B3G3R3
+      uint32_t* o4 = reinterpret_cast<uint32_t*>(o);
+      o4[0] = col[0] | (col[1] << 24);
+      o4[1] = (col[1] >> 8) | (col[2] << 16);
+      o4[2] = (col[2] >> 16) | (col[3] << 8);
     } else {
-      const uint32_t cc[2] = {c0, c1};
-      for (int j = 0; j < 2 && c + j < W; ++j) {
-        o[3 * j] = cc[j] & 255;
-        o[3 * j + 1] = (cc[j] >> 8) & 255;
-        o[3 * j + 2] = (cc[j] >> 16) & 255;
+      for (int j = 0; j < cnt; ++j) {
+        o[3 * j] = col[j] & 255;
+        o[3 * j + 1] = (col[j] >> 8) & 255;
+        o[3 * j + 2] = (col[j] >> 16) & 255;
       }
     }
     if (gray) {
-      const uint32_t cc[2] = {c0, c1};
-      uint32_t g2 = 0;
+      uint32_t g4 = 0;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const uint32_t bb = cc[j] & 255, gg = (cc[j] >> 8) & 255, rr = (cc[j] >> 16) & 255;
-        g2 |= ((1868u * bb + 9617u * gg + 4899u * rr + 8192u) >> 14) << (8 * j);
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t bb = col[j] & 255, gg = (col[j] >> 8) & 255, rr = (col[j] >> 16) & 255;
+        g4 |= ((1868u * bb + 9617u * gg + 4899u * rr + 8192u) >> 14) << (8 * j);
       }
-      if (both && vg) *reinterpret_cast<uint16_t*>(gray + q) = (uint16_t)g2;
-      else for (int j = 0; j < 2 && c + j < W; ++j) gray[q + j] = (g2 >> (8 * j)) & 255;
+      if (cnt == 4 && vg) *reinterpret_cast<uint32_t*>(gray + q) = g4;
+      else for (int j = 0; j < cnt; ++j) gray[q + j] = (g4 >> (8 * j)) & 255;
     }
   }
 }

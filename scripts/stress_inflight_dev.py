@@ -1,6 +1,6 @@
 """Config-5-style stress: K device frames per step (msg_watershed_colorize_batch_dev) with up to
 `inflight` floods in flight; counts steps that raise and frames whose labels differ from the
-same frames flooded one at a time (inflight 1); exit 1 if any.  usage: python scripts/stress_inflight_dev.py [steps] [K] [inflight] [size]"""
+same frames flooded one at a time (inflight 1); exit 1 if any.  usage: python scripts/stress_inflight_dev.py [steps] [K] [inflight] [size] [speculative 0/1]"""
 import os
 import sys
 
@@ -25,6 +25,10 @@ def main():
     labs = [torch.empty_like(m) for m in mks]
     dsts = [torch.empty((S, S, 3), dtype=torch.uint8, device=dev) for _ in fr]
     seg = msegment.Segmenter(0)
+    if len(sys.argv) > 5:
+        seg.set_speculative(bool(int(sys.argv[5])))
+    if os.environ.get("STRESS_DIAG"):
+        seg.set_diag(True)
     seg.set_batch_inflight(1)  # reference labels: one flood at a time on the context itself
     seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)
     torch.cuda.synchronize()
@@ -42,7 +46,10 @@ def main():
         for k in range(K):
             if not torch.equal(ref[k], labs[k]):
                 bad += 1
-                print("step %d frame %d differs" % (s, k), flush=True)
+                d = (ref[k] != labs[k]).nonzero()
+                info = ", ".join("(%d,%d) ref %d got %d" % (int(y), int(x), int(ref[k][y, x]), int(labs[k][y, x]))
+                                 for y, x in d[:4].tolist())
+                print("step %d frame %d differs in %d px: %s" % (s, k, d.shape[0], info), flush=True)
     print("K %d inflight %d size %d: %d error steps, %d bad frames in %d steps" % (K, inflight, S, errs, bad, steps),
           flush=True)
     seg.close()
