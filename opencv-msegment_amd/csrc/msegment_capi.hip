@@ -373,6 +373,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   ws.cflag = c->d_cflag;
   ws.ctl = c->d_ctl;
   ws.diag = c->diag ? c->d_diag : nullptr;
+
   ws.hmir = c->d_mir;
   ws.H = H;
   ws.W = W;
@@ -486,11 +487,6 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   if (tail.error & ERR_TIMEOUT)
     return fail(c, MSG_ETIMEOUT, "in-kernel wait timed out (grid not co-resident?)");
   if (tail.error & ERR_CAPACITY) return fail(c, MSG_ESTATE, "bucket capacity exceeded");
-  if (tail.error & ERR_REPUSH)
-    return fail(c, MSG_ESTATE, "a push found its target already queued or labelled (%llu pushes, first at site %llu: "
-                "labelled %llu, queued %llu; last prev %d dest %u, epoch %u rank %u; flood epochs %u..)", dgv[7], dgv[11], dgv[12], dgv[13],
-                (int)(dgv[14] >> 32), (unsigned)dgv[14], (unsigned)(dgv[15] >> 32), (unsigned)dgv[15],
-                c->epoch - (unsigned)std::min<long long>(tail.batches + 4, 0x7fffffff));
   if (tail.error & ERR_LEFTOVER) {
     unsigned long long lo[8] = {0};
     if (c->diag) {  // classify them (k_leftover_diag) for the message

@@ -720,26 +720,7 @@ __global__ __launch_bounds__(256) void k_compact(Ws ws, int nrc) {
 }
 
 __device__ __forceinline__ int ld_state(const Ws& ws, long long t) { return ws.mk[t]; }
-// Wait until this wave's global stores have completed.  __syncthreads() orders LDS but, as
-// compiled for gfx950 (s_waitcnt lgkmcnt(0); s_barrier), not one wave's global stores before
-// another wave's later global loads: with 8 concurrent floods (scripts/stress_inflight_dev.py,
-// GPU_MAX_HW_QUEUES=16) a small-batch loop's next gather in another wave read a pushed pixel as
-// still unknown and queued it twice.  Used before every barrier that hands global state
-// written by some waves to loads by others within one workgroup.
-__device__ __forceinline__ void stores_done() { __builtin_amdgcn_s_waitcnt(0); }
 
-// Diagnostics (msg_set_diag): a push target must still be unknown (0).  Counts violations by kind
-// and records the first push site that saw one (1 k_scatter, 2 small-batch loop, 3 tiny loop).
-__device__ __noinline__ void check_push(const Ws& ws, long long n, int dest, unsigned epoch, int rank, int site) {
-  const int prev = __hip_atomic_load(ws.mk + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (prev == 0) return;
-  atomicOr(&ws.ctl->error, ERR_REPUSH);
-  atomicAdd(&ws.diag[7], 1ull);
-  atomicAdd(&ws.diag[prev <= -3 ? 13 : 12], 1ull);
-  atomicCAS(&ws.diag[11], 0ull, (unsigned long long)site);
-  ws.diag[14] = ((unsigned long long)(uint32_t)prev << 32) | (uint32_t)dest;
-  ws.diag[15] = ((unsigned long long)epoch << 32) | (uint32_t)rank;
-}
 // 32-bit form of nb_of for indices taken from the margin start (a multiple of 16: tile-aligned)
 __device__ __forceinline__ int nbi(int t, int d, int Wt) {
   const int row = Wt << 4;
@@ -932,21 +913,27 @@ __global__ __launch_bounds__(RBS, 4) void k_resolve(Ws ws) {
   const unsigned long long etag = (unsigned long long)B.epoch << 32;  // final label granule
   const unsigned long long ptag = etag | (1ull << 63);                // provisional base fold
   unsigned long long* const dg = ws.diag;
-  __shared__ int s_skip, s_yield;
+  // s_skip is double-buffered by chunk parity: a wave that skips a chunk reads its flag after
+  // the chunk's barrier, and thread 0 may already be writing the next chunk's flag by then (the
+  // skip path has no second barrier); one buffer let a late wave read the next chunk's flag and
+  // process a completed chunk out of step with the block (re-runs under concurrent floods)
+  __shared__ int s_skip[2], s_yield;
   __shared__ unsigned long long s_ctag;  // this run's chunk claims: {epoch, re-run}
   if (tid == 0) s_ctag = etag | (unsigned)B.rrun;
   if (work && blockIdx.x == 0 && tid == 0) ctl->rsv = B.epoch;  // k_scan commits only decided batches
   if (tid == 0) s_yield = 0;
   for (int base = blockIdx.x * RBS; work && base < B.n; base += gridDim.x * RBS) {
     const int chunk = base / RBS;
+    const int par = (base / (gridDim.x * RBS)) & 1;
     if (tid == 0) {  // claim the chunk, or skip it when an earlier run of this batch completed it
-      s_skip = B.rrun > 0 &&
-               __hip_atomic_load(&ws.cflag[2 * chunk + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == B.epoch;
-      if (!s_skip) __hip_atomic_store(&ws.cflag[2 * chunk], s_ctag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int sk = B.rrun > 0 &&
+                     __hip_atomic_load(&ws.cflag[2 * chunk + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == B.epoch;
+      s_skip[par] = sk;
+      if (!sk) __hip_atomic_store(&ws.cflag[2 * chunk], s_ctag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tid < NQ) hist[tid] = 0;
     __syncthreads();
-    if (s_skip) continue;
+    if (s_skip[par]) continue;
     const int wbase = base + (tid & ~63);
     const int i = wbase + lane;
     const bool valid = i < B.n;
@@ -1160,6 +1147,7 @@ __global__ __launch_bounds__(RBS, 4) void k_resolve(Ws ws) {
     }
     if (tid < NQ && hist[tid]) atomicAdd(&ws.cnt[(long long)(base / CH) * NQ + tid], hist[tid]);
     if (tid == 0) __hip_atomic_store(&ws.cflag[2 * chunk + 1], B.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
   }
   __syncthreads();
   if (tid == 0 && s_minpush < NQ) atomicMin(&ctl->minpush, s_minpush);
@@ -1433,13 +1421,9 @@ __device__ void scatter_chunks(const Ws& ws, const Batch& B, int first, int stri
         continue;
       }
       const long long n = (B.mode == 0) ? nb_of(p, d, Wt) : p;
-      if (ws.diag && B.mode == 0) check_push(ws, n, dest, B.epoch, i0 + tid, 1);
       st_state(ws, n, queued_state(dest));
       ws.qbuf[dest] = (int32_t)n;
     }
-    // the block's own later reads of these states (k_scan's small-batch loop after it) come from
-    // other waves: a barrier alone does not order one wave's stores before another's loads
-    stores_done();
     __syncthreads();  // before the next sub-round reuses run/wcnt
   }
 }
@@ -1614,7 +1598,6 @@ __device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qba
         continue;
       }
       const long long n = nb_of(it.p, d, Wt);
-      if (ws.diag) check_push(ws, n, dest, B.epoch, i, 3);
       st_state(ws, n, queued_state(dest));
       ws.qbuf[dest] = (int32_t)n;
       ++pushed;
@@ -1990,12 +1973,10 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
           continue;
         }
         const long long n = nb_of(p, d, Wt);
-        if (ws.diag) check_push(ws, n, dest, B.epoch, i, 2);
         st_state(ws, n, queued_state(dest));
         ws.qbuf[dest] = (int32_t)n;
         ++pushed;
       }
-      stores_done();  // the next batch's gathers run in other waves (see stores_done)
       __syncthreads();
       if (tid < NQ) {
         s_tail[tid] += s_tot[tid];

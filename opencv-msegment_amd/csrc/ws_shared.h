@@ -59,7 +59,6 @@ constexpr int ERR_TIMEOUT = 1;
 constexpr int ERR_STATE = 2;
 constexpr int ERR_CAPACITY = 4;
 constexpr int ERR_LEFTOVER = 8;  // a queued (or phase-1) state survived the flood (k_untile)
-constexpr int ERR_REPUSH = 16;   // diagnostics: a push found its target already queued or labelled
 
 // Speculative generations (k_spec_round / k_spec_flatten, ws_kernels.hip): the interrupt-dense
 // regime.  A generation is the whole lowest bucket; each item's execution is its own pop plus its

@@ -347,7 +347,7 @@ def test_batch_inflight_more_hw_queues():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
     r = subprocess.run([sys.executable, os.path.join(root, "scripts", "stress_inflight_dev.py"),
-                        "2", "8", "8", "4096"], env=env, capture_output=True, text=True, timeout=110)
+                        "6", "8", "8", "4096"], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "0 error steps, 0 bad frames" in r.stdout
 
@@ -410,6 +410,24 @@ def test_resolve_give_up_and_rerun(seg, kind, S):
         out = gpu_ws(seg, img, m)
     finally:
         seg.set_diag(False)
+    assert np.array_equal(out, ws_oracle.watershed(img, m))
+
+
+@pytest.mark.parametrize("blocks", [4, 16])
+def test_rerun_skips_with_many_chunks_per_block(seg, blocks):
+    """Re-runs on a small k_resolve grid: every block walks many chunks, alternating completed
+    (skipped) and re-run ones.  Regression: the skip flag was one shared word, so a wave that
+    lagged behind a skipped chunk could read the next chunk's flag and redo a completed chunk out
+    of step with its block (wrong bucket histograms, pixels queued twice; found as rare label
+    differences with 8 concurrent floods).  Labels must be the oracle's."""
+    img, m, d = synth.frame("mosaic", 1024, 1024, 9)
+    seg.set_diag(2)
+    seg.set_resolve_grid(blocks)
+    try:
+        out = gpu_ws(seg, img, m)
+    finally:
+        seg.set_diag(False)
+        seg.set_resolve_grid(0)
     assert np.array_equal(out, ws_oracle.watershed(img, m))
 
 
