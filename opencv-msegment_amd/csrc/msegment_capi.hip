@@ -406,7 +406,11 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 16 * sizeof(unsigned long long), st));
   HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)npx * NQ * sizeof(int32_t), st));
   const int nrc = H * ws.nseg;  // raster chunks
-  LAUNCH(c, KID_PREP, st, k_prep, dim3((H + 3) / 4 * ws.nseg), dim3(RSEG), 0, ws, d_mk_in);
+  // k_prep4 (one thread per tile) where widths and buffers allow 12-B / 16-B quad loads
+  if (W % 4 == 0 && ((uintptr_t)d_img & 3) == 0 && ((uintptr_t)d_mk_in & 15) == 0)
+    LAUNCH(c, KID_PREP, st, k_prep4, dim3((H + 3) / 4 * ws.nseg), dim3(PREP4_T), 0, ws, d_mk_in);
+  else
+    LAUNCH(c, KID_PREP, st, k_prep, dim3((H + 3) / 4 * ws.nseg), dim3(RSEG), 0, ws, d_mk_in);
   LAUNCH(c, KID_INIT_SCAN, st, k_init_scan, dim3(1), dim3(1024), 0, ws, nrc, c->epoch, c->stag);
   LAUNCH(c, KID_COMPACT, st, k_compact, dim3((nrc + 4 * CPW - 1) / (4 * CPW)), dim3(256), 0, ws, nrc);
   LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
