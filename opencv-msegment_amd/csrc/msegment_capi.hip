@@ -571,8 +571,9 @@ int run_batch(msg_ctx* c, int n, F fn) {
   int rc = ensure_subs(c, k);
   if (rc) return rc;
   // up to min(k, hardware queues) floods run kernels concurrently (streams beyond the HIP
-  // runtime's hardware queues share them and serialise).  k_resolve deals its rank chunks in
-  // dispatch order, so concurrent grids need not be co-resident: each keeps the full grid.
+  // runtime's hardware queues share them and serialise).  Concurrent k_resolve grids need not be
+  // co-resident (a block waiting on an unclaimed chunk gives its own chunk up and the batch is
+  // re-run, ws_kernels.hip), so each flood keeps the full grid.
   for (int w = 0; w < k; ++w) {
     c->subs[w]->res_grid = c->res_grid;
     c->subs[w]->spec = c->spec;
