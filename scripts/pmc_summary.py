@@ -2,7 +2,9 @@
 """Fold rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs (separate passes) into per-kernel HBM bytes
 per launch.  FETCH_SIZE is doubled: on gfx950 it reports half the bytes of wide coalesced reads
 (MI355X_MICROARCH.md, HBM/rocprofv3 section; checked here on k_untile, whose 16-B-per-lane loads
-move a known 8 B per pixel).  Other read widths (random 4-8 B gathers) are uncalibrated.
+move a known 8 B per pixel).  Random 4-B and 16-B gathers, one per distinct 128-B line, calibrated
+in round 2 (scripts/exp/fetch_calib.hip): TCC_EA0_RDREQ counts one request per line (as for the
+coalesced reads: one per 128-B line) and FETCH_SIZE reads 64 B per line, so the same x2 holds.
 
   python scripts/pmc_summary.py <dir with pmc_FETCH_SIZE/ and pmc_WRITE_SIZE/> <out.json> [note] [bench args]
 
