@@ -383,17 +383,31 @@ __global__ __launch_bounds__(RSEG) void k_prep(Ws ws, const int32_t* __restrict_
 // distances of its tile once each (a tile-row thread recomputed the vertical ones of 3 rows and
 // rebuilt packed pixels in LDS): about half of k_prep's VALU instructions per pixel.  Same
 // outputs, same raster chunks (a block is still a 4-row x RSEG-column strip), same capacity
-// histogram.  Measured 118 -> 110 us at 4096^2 only: both forms wait on memory, not on VALU
-// (PMC: 51% of wave cycles in SQ_WAIT_ANY, 9% VALU-active, ~5 resident waves per CU on average).
+// histogram.  Halving the VALU work alone moved 118 -> 110 us at 4096^2 (PMC: 51% of wave
+// cycles waiting on memory, 9% VALU-active); what bounded it was the write pattern -- a tile per
+// thread stored 16 B per lane at a 64-B stride doubled the HBM writes (283 MB against 128) --
+// so the tiles now go out lane-contiguously through the halo's LDS: 89 us, 138 MB written.
 constexpr int PREP4_T = RSEG / 4;  // threads per block = tiles per strip
 
 struct alignas(4) Quad3 { uint32_t x, y, z; };
 
+// the halo columns while the tiles are computed, then the strip's tiles for the coalesced stores
+union Prep4Lds {
+  struct {
+    uint32_t pf[6][PREP4_T + 2], pb[6][PREP4_T + 2];  // each tile's first / last pixel
+    int32_t mf[6][PREP4_T + 2], mb[6][PREP4_T + 2];   // and their markers
+  } h;
+  int4 tile[4 * PREP4_T];
+};
+
 __global__ __launch_bounds__(PREP4_T) void k_prep4(Ws ws, const int32_t* __restrict__ mk_in) {
   __shared__ unsigned caph[NQ];
-  __shared__ uint32_t s_pf[6][PREP4_T + 2], s_pb[6][PREP4_T + 2];  // each tile's first / last pixel
-  __shared__ int32_t s_mf[6][PREP4_T + 2], s_mb[6][PREP4_T + 2];   // and their markers
+  __shared__ Prep4Lds u;
   __shared__ unsigned long long s_wsum[PREP4_T / 64];
+  auto& s_pf = u.h.pf;
+  auto& s_pb = u.h.pb;
+  auto& s_mf = u.h.mf;
+  auto& s_mb = u.h.mb;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const int H = ws.H, W = ws.W, Wt = ws.Wt;
   const int tr = blockIdx.x / ws.nseg, cs = blockIdx.x % ws.nseg;
@@ -445,20 +459,13 @@ __global__ __launch_bounds__(PREP4_T) void k_prep4(Ws ws, const int32_t* __restr
     }
   }
   __syncthreads();
-  // channels, extracted once: rows 0..5 x 4 pixels, and the halo pixels of rows 1..4
-  uint32_t ch[6][6][3];  // [row][strip column 0..5 = c0 - 1 .. c0 + 4][channel]
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      uint32_t v;
-      if (k == 0) v = (i >= 1 && i <= 4) ? s_pb[i][tid] : 0u;
-      else if (k == 5) v = (i >= 1 && i <= 4) ? s_pf[i][tid + 2] : 0u;
-      else v = px[i][k - 1];
-#pragma unroll
-      for (int cc = 0; cc < 3; ++cc) ch[i][k][cc] = (v >> (8 * cc)) & 255u;
-    }
-  }
+  // distances from packed pixels, channels extracted per use (registers, not VALU, bound the
+  // occupancy of this latency-bound kernel)
+  auto dist = [](uint32_t a, uint32_t b) -> int {
+    const uint32_t pa[3] = {a & 255u, (a >> 8) & 255u, (a >> 16) & 255u};
+    const uint32_t pb[3] = {b & 255u, (b >> 8) & 255u, (b >> 16) & 255u};
+    return (int)linf_ch(pa, pb);
+  };
   int run_w = -1;
   unsigned run_n = 0;
   auto cap_add = [&](int w) {
@@ -470,21 +477,23 @@ __global__ __launch_bounds__(PREP4_T) void k_prep4(Ws ws, const int32_t* __restr
     ++run_n;
   };
   unsigned p1m[4] = {0, 0, 0, 0};
+  int sv[4][4];
+  unsigned wq[4][4];
   if (tin) {
     int vdn[5][4];  // distance between rows i and i + 1 at pixel k
 #pragma unroll
     for (int i = 0; i < 5; ++i)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) vdn[i][k] = (int)linf_ch(ch[i][k + 1], ch[i + 1][k + 1]);
+      for (int k = 0; k < 4; ++k) vdn[i][k] = dist(px[i][k], px[i + 1][k]);
 #pragma unroll
     for (int ry = 0; ry < 4; ++ry) {
       const int r = r0 + ry, i = ry + 1;
       int hd[5];
+      hd[0] = dist(s_pb[i][tid], px[i][0]);
 #pragma unroll
-      for (int k = 0; k < 5; ++k) hd[k] = (int)linf_ch(ch[i][k], ch[i][k + 1]);
+      for (int k = 1; k < 4; ++k) hd[k] = dist(px[i][k - 1], px[i][k]);
+      hd[4] = dist(px[i][3], s_pf[i][tid + 2]);
       const int mlh = s_mb[i][tid], mrh = s_mf[i][tid + 2];
-      int sv[4];
-      unsigned wq[4];
 #pragma unroll
       for (int rx = 0; rx < 4; ++rx) {
         const int c = c0 + rx;
@@ -525,12 +534,9 @@ __global__ __launch_bounds__(PREP4_T) void k_prep4(Ws ws, const int32_t* __restr
             }
           }
         }
-        sv[rx] = state;
-        wq[rx] = w4;
+        sv[ry][rx] = state;
+        wq[ry][rx] = w4;
       }
-      const unsigned to = ((unsigned)(tr * Wt + tc) << 4) + 4u * ry;
-      *reinterpret_cast<int4*>(ws.mk + to) = make_int4(sv[0], sv[1], sv[2], sv[3]);
-      *reinterpret_cast<int4*>(ws.w4 + to) = make_int4((int)wq[0], (int)wq[1], (int)wq[2], (int)wq[3]);
     }
   }
   if (run_n) atomicAdd(&caph[run_w], run_n);
@@ -566,6 +572,28 @@ __global__ __launch_bounds__(PREP4_T) void k_prep4(Ws ws, const int32_t* __restr
   for (int k = tid; k < NQ; k += PREP4_T)
     if (caph[k]) atomicAdd(&ws.capp[(blockIdx.x % CAP_SLOTS) * NQ + k], caph[k]);
   if (tid < 4 && r0 + tid < H) ws.tot[(r0 + tid) * ws.nseg + cs] = (int)((total >> (16 * tid)) & 0xffff);
+  // the strip's tiles are contiguous in mk / w4 (tile-row-major): stored lane-contiguously through
+  // LDS (a tile per thread stored 16 B per lane at a 64-B stride, and the partial lines were
+  // written back separately: 283 MB of HBM writes per 4096^2 frame against 128 MB)
+  const int ntile = min(PREP4_T, Wt - cs * PREP4_T);  // tiles of this strip inside the frame
+  const unsigned base = (unsigned)(tr * Wt + cs * PREP4_T) << 4;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    __syncthreads();  // the halo columns (a = 0) / the previous array's chunks (a = 1) are consumed
+    if (tin) {
+#pragma unroll
+      for (int ry = 0; ry < 4; ++ry)
+        u.tile[4 * tid + ry] = a == 0 ? make_int4(sv[ry][0], sv[ry][1], sv[ry][2], sv[ry][3])
+                                      : make_int4((int)wq[ry][0], (int)wq[ry][1], (int)wq[ry][2], (int)wq[ry][3]);
+    }
+    __syncthreads();
+    int32_t* const dst = a == 0 ? ws.mk : ws.w4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = k * PREP4_T + tid;  // 16-B chunk: tile q / 4, tile row q % 4
+      if (q < 4 * ntile) *reinterpret_cast<int4*>(dst + base + 4u * q) = u.tile[q];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
