@@ -490,3 +490,28 @@ def test_default_stream_ordering_without_device_sync(seg):
         dst_copy = dst.clone()
         assert np.array_equal(lab_copy.cpu().numpy(), want)
         assert np.array_equal(dst_copy.cpu().numpy(), ws_oracle.colorize(want, d, None))
+
+
+@pytest.mark.parametrize("W", [256, 259])
+def test_prep_paths_on_misaligned_device_buffers(seg, W):
+    """k_prep4 (quad loads: width divisible by 4, 4-B aligned BGR, 16-B aligned markers) and the
+    tile-row k_prep (every other case) give the same flood: the same frame through aligned
+    tensors and through tensors offset by one element (which forces k_prep) -- and the oracle."""
+    import torch
+
+    img, m, _ = synth.frame("mosaic_noise", 192, W, 21)
+    want = ws_oracle.watershed(img, m)
+    dev = torch.device("cuda", 0)
+    outs = []
+    for off in (0, 1):
+        bimg = torch.zeros(img.size + 3 * off, dtype=torch.uint8, device=dev)
+        bmk = torch.zeros(m.size + off, dtype=torch.int32, device=dev)
+        timg = bimg[3 * off:].view(img.shape)
+        tmk = bmk[off:].view(m.shape)
+        timg.copy_(torch.from_numpy(img))
+        tmk.copy_(torch.from_numpy(m))
+        lab = torch.empty_like(tmk)
+        seg.watershed_dev(timg, tmk, lab)
+        torch.cuda.synchronize()
+        outs.append(lab.cpu().numpy())
+    assert np.array_equal(outs[0], want) and np.array_equal(outs[1], want)
