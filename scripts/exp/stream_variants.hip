@@ -215,6 +215,88 @@ __global__ __launch_bounds__(256) void kews2(const uint8_t* __restrict__ img, ui
   }
 }
 
+// product layout (R = 1) with nontemporal output stores
+__global__ __launch_bounds__(512) void kews_nt(const uint8_t* __restrict__ img, uint8_t* __restrict__ wr,
+                                               uint8_t* __restrict__ wd, int H, int W) {
+  const unsigned segs = (unsigned)W >> 4;
+  unsigned b = blockIdx.x;
+  const unsigned per_xcd = gridDim.x / 8;
+  if (b < per_xcd * 8) b = (b % 8) * per_xcd + b / 8;
+  const unsigned t = b * blockDim.x + threadIdx.x;
+  if (t >= (unsigned)H * segs) return;
+  const unsigned st = t / segs, sx = t - st * segs;
+  const int r = (int)st;
+  const bool has_r = sx + 1 < segs;
+  uint32_t rows[2][13];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int k = 0; k < 13; ++k) rows[i][k] = 0;
+    if (r + i < H) {
+      const unsigned p0 = (unsigned)(r + i) * (unsigned)W + 16u * sx;
+      msg::ld48(img + 3u * p0, rows[i]);
+      if (has_r && i == 0) rows[i][12] = *reinterpret_cast<const uint32_t*>(img + 3u * (p0 + 16u));
+    }
+  }
+  uint32_t cur[17][3], nxt[17][3];
+  msg::unpack17(rows[0], cur);
+  msg::unpack17(rows[1], nxt);
+  const bool has_d = r + 1 < H;
+  uint32_t orr[4] = {0, 0, 0, 0}, odd[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t vr = (k < 15 || has_r) ? msg::linf_ch(cur[k], cur[k + 1]) : 0u;
+    const uint32_t vd = has_d ? msg::linf_ch(cur[k], nxt[k]) : 0u;
+    orr[k >> 2] |= vr << (8 * (k & 3));
+    odd[k >> 2] |= vd << (8 * (k & 3));
+  }
+  typedef unsigned u4v __attribute__((ext_vector_type(4)));
+  const unsigned p0 = (unsigned)r * (unsigned)W + 16u * sx;
+  u4v a = {orr[0], orr[1], orr[2], orr[3]}, c = {odd[0], odd[1], odd[2], odd[3]};
+  __builtin_nontemporal_store(a, reinterpret_cast<u4v*>(wr + p0));
+  __builtin_nontemporal_store(c, reinterpret_cast<u4v*>(wd + p0));
+}
+
+// the product kernel (R = 1) under other block sizes
+__global__ __launch_bounds__(1024) void kews_bs(const uint8_t* __restrict__ img, uint8_t* __restrict__ wr,
+                                                uint8_t* __restrict__ wd, int H, int W) {
+  const unsigned segs = (unsigned)W >> 4;
+  unsigned b = blockIdx.x;
+  const unsigned per_xcd = gridDim.x / 8;
+  if (b < per_xcd * 8) b = (b % 8) * per_xcd + b / 8;
+  const unsigned t = b * blockDim.x + threadIdx.x;
+  if (t >= (unsigned)H * segs) return;
+  const unsigned st = t / segs, sx = t - st * segs;
+  const int r = (int)st;
+  const bool has_r = sx + 1 < segs;
+  uint32_t rows[2][13];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int k = 0; k < 13; ++k) rows[i][k] = 0;
+    if (r + i < H) {
+      const unsigned p0 = (unsigned)(r + i) * (unsigned)W + 16u * sx;
+      msg::ld48(img + 3u * p0, rows[i]);
+      if (has_r && i == 0) rows[i][12] = *reinterpret_cast<const uint32_t*>(img + 3u * (p0 + 16u));
+    }
+  }
+  uint32_t cur[17][3], nxt[17][3];
+  msg::unpack17(rows[0], cur);
+  msg::unpack17(rows[1], nxt);
+  const bool has_d = r + 1 < H;
+  uint32_t orr[4] = {0, 0, 0, 0}, odd[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t vr = (k < 15 || has_r) ? msg::linf_ch(cur[k], cur[k + 1]) : 0u;
+    const uint32_t vd = has_d ? msg::linf_ch(cur[k], nxt[k]) : 0u;
+    orr[k >> 2] |= vr << (8 * (k & 3));
+    odd[k >> 2] |= vd << (8 * (k & 3));
+  }
+  const unsigned p0 = (unsigned)r * (unsigned)W + 16u * sx;
+  *reinterpret_cast<uint4*>(wr + p0) = make_uint4(orr[0], orr[1], orr[2], orr[3]);
+  *reinterpret_cast<uint4*>(wd + p0) = make_uint4(odd[0], odd[1], odd[2], odd[3]);
+}
+
 // untile: lane = one tile row (16 B of states); labels as one 16-B store, colours as 12 B
 template <bool NT>
 __global__ __launch_bounds__(256) void unt(const int32_t* __restrict__ mk, int H, int W, int Wt,
@@ -273,8 +355,7 @@ int main(int argc, char** argv) {
   }
   struct V { const char* name; ewfn f; int R; } vars[] = {{"ewq<2>", ewq<2, false>, 2}};
   struct VS { const char* name; ewfn f; int R; } svars[] = {
-      {"prod<1>", msg::k_edge_weights16<1>, 1}, {"prod<4>", msg::k_edge_weights16<4>, 4},
-      {"kews2<1>", kews2<1>, 1}, {"kews2<2>", kews2<2>, 2}};
+      {"prod<1>", msg::k_edge_weights16<1>, 1}, {"prod<2>", msg::k_edge_weights16<2>, 2}};
   for (auto& v : svars) {
     CK(hipMemset(wr, 0x55, N)); CK(hipMemset(wd, 0x55, N));
     const long long th = (long long)((S + v.R - 1) / v.R) * (S / 16);
@@ -284,6 +365,15 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(C.data(), wr, N, hipMemcpyDeviceToHost)); CK(hipMemcpy(D.data(), wd, N, hipMemcpyDeviceToHost));
     printf("%-10s %s\n", v.name, (memcmp(A.data(), C.data(), N) == 0 && memcmp(B.data(), D.data(), N) == 0) ? "same" : "DIFFERENT");
   }
+  for (int bs : {64, 128, 512, 1024}) {
+    CK(hipMemset(wr, 0x55, N)); CK(hipMemset(wd, 0x55, N));
+    const long long th = (long long)S * (S / 16);
+    for (int i = 0; i < reps; ++i)
+      hipLaunchKernelGGL(kews_bs, dim3((unsigned)((th + bs - 1) / bs)), dim3(bs), 0, 0, img, wr, wd, S, S);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(C.data(), wr, N, hipMemcpyDeviceToHost)); CK(hipMemcpy(D.data(), wd, N, hipMemcpyDeviceToHost));
+    printf("kews_bs/%d %s\n", bs, (memcmp(A.data(), C.data(), N) == 0 && memcmp(B.data(), D.data(), N) == 0) ? "same" : "DIFFERENT");
+  }
   for (auto& v : vars) {
     CK(hipMemset(wr, 0x55, N)); CK(hipMemset(wd, 0x55, N));
     const long long th = (long long)((S + v.R - 1) / v.R) * (S / 4);
@@ -292,6 +382,15 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(C.data(), wr, N, hipMemcpyDeviceToHost)); CK(hipMemcpy(D.data(), wd, N, hipMemcpyDeviceToHost));
     printf("%-10s %s\n", v.name, (memcmp(A.data(), C.data(), N) == 0 && memcmp(B.data(), D.data(), N) == 0) ? "same" : "DIFFERENT");
+  }
+  for (int bs : {64, 128, 512, 1024}) {
+    CK(hipMemset(wr, 0x55, N)); CK(hipMemset(wd, 0x55, N));
+    const long long th = (long long)S * (S / 16);
+    for (int i = 0; i < reps; ++i)
+      hipLaunchKernelGGL(kews_bs, dim3((unsigned)((th + bs - 1) / bs)), dim3(bs), 0, 0, img, wr, wd, S, S);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(C.data(), wr, N, hipMemcpyDeviceToHost)); CK(hipMemcpy(D.data(), wd, N, hipMemcpyDeviceToHost));
+    printf("kews_bs/%d %s\n", bs, (memcmp(A.data(), C.data(), N) == 0 && memcmp(B.data(), D.data(), N) == 0) ? "same" : "DIFFERENT");
   }
   // untile
   const int Wt = (S + 3) / 4, Ht = (S + 3) / 4;
