@@ -9,6 +9,8 @@ through libmsegment's device entry point msg_watershed_colorize_dev.
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python bench.py --pipeline nc [--kind mosaic_noise]   # notConnectedMarkers'
       marker stage (gray + histogram -> levels -> markers) + watershed + colorByIndexes per step
+  python bench.py --pipeline color                      # colorAutoMarkerWatershed's
+      marker stage (sharpen, Otsu, chamfer distance, contours) + the flood of the sharpened frame
 
 N > 1 (launched by torch.distributed.run, one rank per GPU): every rank segments its own frame
 (BASELINE config 5: batched frames, one per GPU, no collectives -- weak scaling).  The only
@@ -41,6 +43,7 @@ sys.path.insert(0, os.path.join(ROOT, "opencv-msegment_amd"))
 METRIC = "Mpixels/sec segmented at {S}x{S} RGB; achieved HBM GB/s vs peak"  # BASELINE.json at S = 4096
 METRIC_NC = "Mpixels/sec segmented by notConnectedMarkers (marker stage + watershed + colorByIndexes)"
 METRIC_SHAPE = "Mpixels/sec segmented by shapeAutoMarkerWatershed (marker stage + watershed + colorByIndexes)"
+METRIC_COLOR = "Mpixels/sec segmented by colorAutoMarkerWatershed (marker stage + watershed + colorByIndexes)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
 # Algorithmic bytes (DESIGN.md "Kernels"): what each kernel must move at minimum per unit.
@@ -195,6 +198,28 @@ def cpu_baseline_shape(img, budget_s=12.0, max_reps=10, rows=512):
             "sample": "%d band(s) of %dx%d (median %d as for the full frame): oracle/shape_oracle.py "
                       "marker stage (numpy/scipy) + ws_oracle.c watershed + colorize, 1 thread, %.1f s"
                       % (reps, H, W, k, t_tot)}, None
+
+
+def cpu_baseline_color(img, budget_s=12.0, max_reps=10, rows=512):
+    """The oracles of the colour pipeline (numpy + C chamfer marker stage, the C flood) on a band of
+    the frame (its first `rows` rows), bounded to ~budget_s."""
+    import numpy as np
+
+    from oracle import color_oracle, ws_oracle
+
+    img = np.ascontiguousarray(img[:rows])
+    H, W = img.shape[:2]
+    reps, t_tot = 0, 0.0
+    while reps < max_reps and t_tot < budget_s:
+        t0 = time.perf_counter()
+        sharp, mk, depth = color_oracle.color_markers(img)
+        lab = ws_oracle.watershed(sharp, mk)
+        ws_oracle.colorize(lab, depth, None)
+        t_tot += time.perf_counter() - t0
+        reps += 1
+    return {"value": round(H * W * reps / t_tot / 1e6, 3), "unit": "Mpx/s", "cores": 1, "kind": "port",
+            "sample": "%d band(s) of %dx%d: oracle/color_oracle.py marker stage (numpy/scipy, C chamfer) + "
+                      "ws_oracle.c watershed + colorize, 1 thread, %.1f s" % (reps, H, W, t_tot)}, None
 
 
 def batch_throughput(seg, args, S, seed, sync, steps=5, warmup=2):
@@ -398,7 +423,7 @@ def main(argv=None):
                     help="floods kept in flight together when --frames > 1")
     ap.add_argument("--batch-frames", type=int, default=8,
                     help="frames of the extra 'batch' measurement (config 5 per GPU); 0/1 = skip")
-    ap.add_argument("--pipeline", default="watershed", choices=["watershed", "nc", "shape"],
+    ap.add_argument("--pipeline", default="watershed", choices=["watershed", "nc", "shape", "color"],
                     help="nc: notConnectedMarkers' marker stage builds the seeds each step; "
                          "shape: shapeAutoMarkerWatershed's (median, Canny, rings, components)")
     ap.add_argument("--nc-depth", type=int, default=4, help="user depth of the nc pipeline")
@@ -410,9 +435,9 @@ def main(argv=None):
     args = ap.parse_args(argv)
     # the nc pipeline's scattered seeds put the flood in its slowest regime
     if args.steps is None:
-        args.steps = 2 if args.pipeline == "nc" else 10
+        args.steps = 2 if args.pipeline in ("nc", "color") else 10
     if args.warmup is None:
-        args.warmup = 1 if args.pipeline == "nc" else 3
+        args.warmup = 1 if args.pipeline in ("nc", "color") else 3
 
     if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         raise SystemExit(spawn_ranks(args.gpus, sys.argv[1:] if argv is None else argv))
@@ -492,6 +517,20 @@ def main(argv=None):
             seg.watershed_colorize_dev(t_img, t_lab, t_lab, d, None, t_dst)
 
         step = step1
+    COLOR = args.pipeline == "color"
+    if COLOR:
+        if K > 1:
+            raise SystemExit("--pipeline color runs one frame per step")
+        color_depth = []
+        t_sharp = torch.empty_like(t_img)
+
+        def step1():  # noqa: F811
+            d = seg.color_markers_dev(t_img, t_sharp, t_lab)
+            color_depth[:] = [d]
+            seg.watershed_colorize_dev(t_sharp, t_lab, t_lab, d, None, t_dst)
+
+        step = step1
+    MARKERS = NC or SHAPE or COLOR  # a marker stage before the flood: no digest, no side lines
 
     for _ in range(args.warmup):
         step()
@@ -500,7 +539,7 @@ def main(argv=None):
     parity = None
     dgs = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
     dkey = "%s_%dx%d_s%d" % (args.kind, S, S, seed)
-    if rank == 0 and dkey in dgs and not NC and not SHAPE:  # committed oracle digest of this frame
+    if rank == 0 and dkey in dgs and not MARKERS:  # committed oracle digest of this frame
         got = hashlib.sha256(t_lab.cpu().numpy().tobytes()).hexdigest()
         parity = ("bit-exact vs oracle digest" if got == dgs[dkey]["labels_sha256"]
                   else "MISMATCH vs oracle digest") + " " + dkey
@@ -524,22 +563,22 @@ def main(argv=None):
         kern = kernel_roofline(prof, st if K == 1 else seg.stats(), S * S, args.steps)
 
     stencil = None
-    if not NC and not SHAPE and K == 1:
+    if not MARKERS and K == 1:
         stencil = colour_distance(seg, t_img, img, S, sync, pmc_cfg, check=(rank == 0))
 
     batch = None
-    if K == 1 and not NC and not SHAPE and args.batch_frames > 1:
+    if K == 1 and not MARKERS and args.batch_frames > 1:
         bseed = 100 + rank * args.batch_frames
         batch = batch_throughput(seg, args, S, bseed, sync)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             batch["cpu_baseline"] = cpu_baseline_batch(args.kind, S, bseed, args.batch_frames)
 
     stress = None
-    if rank == 0 and world == 1 and K == 1 and not NC and not SHAPE and args.kind == "mosaic" and args.stress_steps > 0:
+    if rank == 0 and world == 1 and K == 1 and not MARKERS and args.kind == "mosaic" and args.stress_steps > 0:
         stress = stress_line(seg, S, sync, dev, args.stress_steps, cpu=not args.no_cpu_baseline)
 
     pcie = None
-    if rank == 0 and world == 1 and not NC and not SHAPE:
+    if rank == 0 and world == 1 and not MARKERS:
         # host-buffer entry point (what the JNI shim calls): H2D + flood + colourise + D2H
         reps, t_host = 3, 0.0
         for _ in range(reps):
@@ -554,6 +593,8 @@ def main(argv=None):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if SHAPE:
             cpu, cpu_lab = cpu_baseline_shape(img)
+        elif COLOR:
+            cpu, cpu_lab = cpu_baseline_color(img)
         elif NC:
             cpu, cpu_lab = cpu_baseline_nc(img, args.nc_depth, nc_opts)
         else:
@@ -576,7 +617,8 @@ def main(argv=None):
                     "alg_bytes_per_launch": top["alg_bytes_per_launch"], "avg_launch_us": top["avg_us"]}
         e2e_gbs = value * 1e6 * E2E_BYTES_PER_PIXEL / 1e9
         out = {
-            "metric": METRIC_SHAPE if SHAPE else METRIC_NC if NC else METRIC.format(S=S), "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world,
+            "metric": (METRIC_SHAPE if SHAPE else METRIC_NC if NC else METRIC_COLOR if COLOR
+                       else METRIC.format(S=S)), "value": round(value, 3), "unit": "Mpx/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (msegment.synth %s, splitmix64; regenerated on the box)" % args.kind,
@@ -588,6 +630,8 @@ def main(argv=None):
                                        % (args.nc_depth, "+".join(nc_opts) or "no options", len(nc_levels)))
                                       if NC else ("shapeAutoMarkerWatershed marker stage (median %d, depth %d) "
                                                   "+ watershed" % (seg_blur_k, shape_depth[0])) if SHAPE
+                                      else ("colorAutoMarkerWatershed marker stage (depth %d) + watershed of "
+                                            "the sharpened frame" % color_depth[0]) if COLOR
                                       else "watershed",
                                       ({1024: "2", 16384: "4 frame on one GPU"}.get(S, "3") if K == 1
                                        else "5 batching") if world == 1 else "5"),
