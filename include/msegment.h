@@ -69,7 +69,7 @@ typedef struct msg_stats {
     int64_t spec_fallbacks;     /* overflowing executions handed to serial pops                 */
 } msg_stats;
 
-#define MSG_NKERNELS 21
+#define MSG_NKERNELS 22
 typedef struct msg_kernel_profile {
     char    name[32];       /* kernel name, e.g. "k_resolve"                                   */
     int64_t launches;       /* launches timed since the last reset                              */
@@ -177,8 +177,12 @@ int msg_edge_weights_dev(msg_ctx* ctx, const void* d_bgr, void* d_wright, void* 
                                    multi-Otsu split of the 128-bin histogram (:650-722)     */
 #define MSG_NC_MEDIAN_BLUR 0x4u /* AlgorithmOptions.MEDIAN_BLUR: medianBlur(srcGray, k) before
                                    the histogram (:481-483); k = filterMaskSize in option
-                                   bits 8-15 (MSG_NC_MASK(k)), odd, else MSG_EINVAL.  The
-                                   BILATERIAL branch (:487-494) is not provided.             */
+                                   bits 8-15 (MSG_NC_MASK(k)), odd, else MSG_EINVAL.         */
+#define MSG_NC_BILATERAL 0x8u   /* AlgorithmOptions.BILATERIAL (ignored with MEDIAN_BLUR: the
+                                   reference's else-if): bilateralFilter(srcGray, dst, d, 2d, 2d)
+                                   before the histogram (:488-495), d = MSG_NC_MASK's bits,
+                                   BORDER_REFLECT_101, fp32 as OpenCV 3.4.2's non-IPP 8-bit
+                                   path sums it (an IPP build may round pixels differently). */
 #define MSG_NC_MASK(k) (((unsigned)(k) & 0xffu) << 8)
 
 typedef struct msg_bright_level {  /* model/BrightLevel.java */
@@ -211,7 +215,8 @@ int msg_nc_marker_lut(const msg_bright_level* levels, int n_levels, unsigned opt
 int msg_nc_markers_dev(msg_ctx* ctx, const void* d_gray, int rows, int cols,
                        const int32_t* lut256, void* d_markers, void* stream);
 
-/* The whole marker stage: gray (MSG_NC_MEDIAN_BLUR: then its k x k median) + histogram ->
+/* The whole marker stage: gray (MSG_NC_MEDIAN_BLUR: then its k x k median; MSG_NC_BILATERAL:
+ * then its bilateral filter) + histogram ->
  * levels -> markers.  d_gray (the final srcGray) may be NULL (context scratch).  The level count is the watershed depth the reference then uses (:834): draw the
  * palettes for it and call msg_watershed_colorize_dev(d_bgr, d_markers, ...). */
 int msg_nc_marker_stage_dev(msg_ctx* ctx, const void* d_bgr, int rows, int cols, int depth,

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstddef>
@@ -96,6 +97,11 @@ struct msg_ctx {
   long long gscr_n = 0;
   uint8_t* d_gscr2 = nullptr;  // unblurred gray of the NC MEDIAN_BLUR branch
   long long gscr2_n = 0;
+  // NC BILATERIAL branch: the disc of taps (device copy and the host table it is uploaded from,
+  // kept until the stage's histogram read-back has synchronised the stream)
+  BilTap* d_btaps = nullptr;
+  long long btaps_n = 0;
+  std::vector<BilTap> h_btaps;
   // shape marker stage: 6 byte planes, 2 int planes (parents, block keys), 2 block-key arrays,
   // scan scratch, 4 counters
   long long sh_n = 0, sh_nb = 0;
@@ -117,14 +123,14 @@ namespace {
 enum KernelId { KID_PREP, KID_INIT_SCAN, KID_COMPACT, KID_RESOLVE, KID_SCAN, KID_SCATTER,
                 KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_GRAY_HIST, KID_NC_MARKERS, KID_SPEC_ROUND,
                 KID_GRAY, KID_MEDIAN, KID_CANNY, KID_CCL, KID_RING, KID_NUMBER, KID_HOLES, KID_SPEC_FLATTEN,
-                KID_COLOR };
+                KID_COLOR, KID_BILATERAL };
 const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_compact", "k_resolve",
                                                 "k_scan", "k_scatter", "k_colorize",
                                                 "k_edge_weights", "k_untile", "k_gray_hist",
                                                 "k_nc_markers", "k_spec_round", "k_gray",
                                                 "k_median", "k_canny_nms", "k_ccl", "k_ring_median3",
                                                 "k_cc_number", "k_holes", "k_spec_flatten",
-                                                "k_color_stage"};
+                                                "k_color_stage", "k_bilateral"};
 
 hipEvent_t pool_event(msg_ctx* c) {
   if (c->evused == c->evpool.size()) {
@@ -819,6 +825,7 @@ void msg_destroy(msg_ctx* c) {
   dfree(c->d_hist);
   dfree(c->d_gscr);
   dfree(c->d_gscr2);
+  dfree(c->d_btaps);
   dfree(c->d_sh8);
   dfree(c->d_sh32);
   dfree(c->d_shF);
@@ -1155,6 +1162,53 @@ int msg_nc_markers_dev(msg_ctx* c, const void* d_gray, int rows, int cols, const
   return nc_markers(c, (const uint8_t*)d_gray, N, lut256, (int32_t*)d_markers, st);
 }
 
+// The BILATERIAL branch's gray -> bilateral pass into g (N > 0: gray into the scratch plane, then
+// k_bilateral).  The set-up restates bilateralFilter_8u's (OpenCV 3.4.2 imgproc): sigmas
+// 2d <= 0 become 1, radius = d / 2 (d <= 0: cvRound(1.5 sigma_space)), at least 1, colour
+// weights (float)exp(i^2 c), taps (dy, dx, (float)exp(r^2 s)) for r = sqrt(dy^2 + dx^2) <= radius
+// in row-major order.  The tap table's host copy stays in the context: the caller's histogram
+// read-back synchronises the stream before the next call can overwrite it.
+static int nc_bilateral(msg_ctx* c, const uint8_t* d_bgr, int rows, int cols, int d, uint8_t* g,
+                 hipStream_t st) {
+  const long long N = (long long)rows * cols;
+  double sc = 2.0 * d, ss = 2.0 * d;
+  if (sc <= 0) sc = 1;
+  if (ss <= 0) ss = 1;
+  const double gcc = -0.5 / (sc * sc), gsc = -0.5 / (ss * ss);
+  int radius = d <= 0 ? (int)std::nearbyint(ss * 1.5) : d / 2;
+  radius = std::max(radius, 1);
+  BilColor cw;
+  for (int i = 0; i < 256; ++i) cw.v[i] = (float)std::exp(i * i * gcc);
+  c->h_btaps.clear();
+  for (int i = -radius; i <= radius; ++i)
+    for (int j = -radius; j <= radius; ++j) {
+      const double r = std::sqrt((double)i * i + (double)j * j);
+      if (r > radius) continue;
+      c->h_btaps.push_back(BilTap{(float)std::exp(r * r * gsc), i, j});
+    }
+  const long long maxk = (long long)c->h_btaps.size();
+  if (N == 0) return MSG_OK;
+  if (c->btaps_n < maxk) {
+    dfree(c->d_btaps);
+    c->btaps_n = 0;
+    HIPCHK(c, hipMalloc((void**)&c->d_btaps, maxk * sizeof(BilTap)));
+    c->btaps_n = maxk;
+  }
+  if (c->gscr2_n < N) {
+    dfree(c->d_gscr2);
+    c->gscr2_n = 0;
+    HIPCHK(c, hipMalloc((void**)&c->d_gscr2, N + 16));
+    c->gscr2_n = N;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_btaps, c->h_btaps.data(), maxk * sizeof(BilTap), hipMemcpyHostToDevice, st));
+  const int grid = (int)std::max<long long>(1, std::min<long long>(8192, (N + 255) / 256));
+  LAUNCH(c, KID_GRAY, st, k_gray, dim3(grid), dim3(256), 0, d_bgr, N, c->d_gscr2);
+  LAUNCH(c, KID_BILATERAL, st, k_bilateral, dim3((cols + 63) / 64, (rows + BIL_ROWS - 1) / BIL_ROWS),
+         dim3(64 * BIL_ROWS), 0, c->d_gscr2, g, rows, cols, c->d_btaps, (int)maxk, radius, cw);
+  HIPCHK(c, hipGetLastError());
+  return MSG_OK;
+}
+
 int msg_nc_marker_stage_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, int depth,
                             unsigned options, void* d_gray, void* d_markers,
                             msg_bright_level* levels, int max_levels, int* n_levels,
@@ -1205,6 +1259,11 @@ int msg_nc_marker_stage_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, i
         HIPCHK(c, hipMemcpyAsync(g, c->d_gscr2, N, hipMemcpyDeviceToDevice, st));
       HIPCHK(c, hipGetLastError());
     }
+    rc = gray_hist(c, g, N, nullptr, hist, st, true);
+  } else if (options & MSG_NC_BILATERAL) {
+    // bilateralFilter(srcGray, dst, d, 2d, 2d) (:488-495), then the histogram of dst
+    rc = nc_bilateral(c, (const uint8_t*)d_bgr, rows, cols, (int)((options >> 8) & 0xffu), g, st);
+    if (rc) return rc;
     rc = gray_hist(c, g, N, nullptr, hist, st, true);
   } else {
     rc = gray_hist(c, (const uint8_t*)d_bgr, N, g, hist, st);

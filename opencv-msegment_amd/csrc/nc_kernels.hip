@@ -142,4 +142,74 @@ __global__ __launch_bounds__(256) void k_nc_markers(const uint8_t* __restrict__ 
   }
 }
 
+// ---- BILATERIAL pre-filter: bilateralFilter(srcGray, dst, d, 2d, 2d) (:488-495) -------------
+// OpenCV 3.4.2's bilateralFilter_8u for one channel, BORDER_REFLECT_101, in fp32 with the
+// summation order of its x86 (SSE3) path: taps in groups of four, each group's weights and
+// weighted values added pairwise ((0+1)+(2+3)) into the running sums, the last maxk % 4 taps one
+// at a time, dst = cvRound(sum / wsum).  The tables are computed on the host with the same
+// double-precision exp as OpenCV's set-up (the colour table goes to LDS, the taps are read with
+// scalar loads: every lane walks the same disc).  One thread = one pixel, a wave = 64 columns of
+// a row, so each tap's gather is one coalesced 64-byte row segment; blocks whose disc stays
+// inside the frame skip the reflection.  No contraction into FMAs: the products round first.
+struct BilColor {
+  float v[256];
+};
+struct BilTap {
+  float w;
+  int dy, dx;
+};
+constexpr int BIL_ROWS = 4;  // block = 64 columns x 4 rows
+
+__device__ __forceinline__ int reflect101(int p, int n) {  // borderInterpolate, REFLECT_101
+  if ((unsigned)p < (unsigned)n) return p;
+  if (n == 1) return 0;
+  do {
+    p = p < 0 ? -p : 2 * n - 2 - p;
+  } while ((unsigned)p >= (unsigned)n);
+  return p;
+}
+
+__global__ __launch_bounds__(64 * BIL_ROWS) void k_bilateral(const uint8_t* __restrict__ src,
+                                                             uint8_t* __restrict__ dst, int H, int W,
+                                                             const BilTap* __restrict__ taps,
+                                                             int maxk, int radius, BilColor cw) {
+#pragma clang fp contract(off)
+  __shared__ float scw[256];
+  scw[threadIdx.x] = cw.v[threadIdx.x];
+  __syncthreads();
+  const int x0 = blockIdx.x * 64, y0 = blockIdx.y * BIL_ROWS;
+  const int x = x0 + (threadIdx.x & 63), y = y0 + (int)(threadIdx.x >> 6);
+  if (x >= W || y >= H) return;
+  const bool inside = x0 >= radius && y0 >= radius && x0 + 64 + radius <= W && y0 + BIL_ROWS + radius <= H;
+  const int v0 = src[(size_t)y * W + x];
+  auto sample = [&](const BilTap& t, float& w, float& p) {
+    int yy = y + t.dy, xx = x + t.dx;
+    if (!inside) {
+      yy = reflect101(yy, H);
+      xx = reflect101(xx, W);
+    }
+    const int v = src[(size_t)yy * W + xx];
+    w = scw[abs(v - v0)] * t.w;
+    p = w * (float)v;
+  };
+  float sum = 0.f, wsum = 0.f;
+  int k = 0;
+  for (; k + 4 <= maxk; k += 4) {
+    float w0, w1, w2, w3, p0, p1, p2, p3;
+    sample(taps[k], w0, p0);
+    sample(taps[k + 1], w1, p1);
+    sample(taps[k + 2], w2, p2);
+    sample(taps[k + 3], w3, p3);
+    wsum += (w0 + w1) + (w2 + w3);
+    sum += (p0 + p1) + (p2 + p3);
+  }
+  for (; k < maxk; ++k) {
+    float w, p;
+    sample(taps[k], w, p);
+    sum += p;
+    wsum += w;
+  }
+  dst[(size_t)y * W + x] = (uint8_t)__float2int_rn(__fdiv_rn(sum, wsum));
+}
+
 }  // namespace msg

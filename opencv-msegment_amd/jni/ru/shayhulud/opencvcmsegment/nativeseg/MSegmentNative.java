@@ -35,9 +35,12 @@ public final class MSegmentNative {
     private static native int ncMarkers(long ctx, byte[] bgr, int rows, int cols, int depth, int options,
                                         int[] markers, int[] levelsOut);
 
-    /** AlgorithmOptions.GISTO_DIAP / MULTI_OTSU bits of msg_nc_marker_stage (msegment.h). */
+    /** AlgorithmOptions.GISTO_DIAP / MULTI_OTSU / MEDIAN_BLUR / BILATERIAL bits of
+     *  msg_nc_marker_stage (msegment.h); the pre-filters take filterMaskSize in bits 8-15. */
     public static final int NC_GISTO_DIAP = 0x1;
     public static final int NC_MULTI_OTSU = 0x2;
+    public static final int NC_MEDIAN_BLUR = 0x4;
+    public static final int NC_BILATERAL = 0x8;
 
     /**
      * Drop-in for the marker stage of PictureService.notConnectedMarkers (PictureService.java:476-828):

@@ -24,6 +24,7 @@ MSG_ERANGE = -6
 MSG_NC_GISTO_DIAP = 0x1
 MSG_NC_MULTI_OTSU = 0x2
 MSG_NC_MEDIAN_BLUR = 0x4
+MSG_NC_BILATERAL = 0x8
 
 
 def MSG_NC_MASK(k):

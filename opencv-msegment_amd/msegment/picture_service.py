@@ -71,8 +71,9 @@ class PictureService:
         GISTO_DIAP, MULTI_OTSU and MEDIAN_BLUR change the result; NO_SAVE_STEPS / BW_RESULT only
         concern saving step images, which is not part of this drop-in (every step image is
         skipped).  MEDIAN_BLUR = medianBlur(srcGray, filter_mask_size) before the histogram
-        (:481-483; an even size raises MsegError(EINVAL), like medianBlur's assertion).
-        BILATERIAL (:487-494, a floating-point bilateralFilter) raises MsegError(EINVAL).
+        (:481-483; an even size raises MsegError(EINVAL), like medianBlur's assertion); else
+        BILATERIAL = bilateralFilter(srcGray, dst, filter_mask_size, 2 filter_mask_size,
+        2 filter_mask_size) (:488-495, fp32 as OpenCV 3.4.2's non-IPP path sums it).
 
         Same Random draws as the reference: colorByIndexes(markers, n, true) for the
         "colored_markers_summ" step (:830) draws n colours before the watershed's own
@@ -86,12 +87,14 @@ class PictureService:
         from . import MsegError, _lib
 
         opts = set(options)
-        if "BILATERIAL" in opts and "MEDIAN_BLUR" not in opts:  # MEDIAN_BLUR wins (if / else if)
-            raise MsegError(_lib.MSG_EINVAL, "BILATERIAL pre-filter not supported")
         flags = (_lib.MSG_NC_GISTO_DIAP if "GISTO_DIAP" in opts else 0) | (
             _lib.MSG_NC_MULTI_OTSU if "MULTI_OTSU" in opts else 0)
-        if "MEDIAN_BLUR" in opts:
+        if "MEDIAN_BLUR" in opts:  # MEDIAN_BLUR wins (if / else if, :481 / :488)
             flags |= _lib.MSG_NC_MEDIAN_BLUR | _lib.MSG_NC_MASK(filter_mask_size)
+        elif "BILATERIAL" in opts:
+            if not 0 <= int(filter_mask_size) <= 255:
+                raise MsegError(_lib.MSG_EINVAL, "BILATERIAL mask size %d: 0..255" % filter_mask_size)
+            flags |= _lib.MSG_NC_BILATERAL | _lib.MSG_NC_MASK(filter_mask_size)
         colored = "COLORED" in opts
         src = np.ascontiguousarray(np.asarray(src, dtype=np.uint8))
         H, W = src.shape[:2]

@@ -14,6 +14,8 @@ statement, in plain Python with Java's semantics made explicit:
   multi_otsu()       the MULTI_OTSU override + otsuPart                   :650-722, :945-996
   marker_lut()       "ALLOCATE TO LAYERS" + the marker-map sum            :781-828
   markers()          lut[gray]
+  bilateral()        the BILATERIAL pre-filter bilateralFilter(srcGray, d, 2d, 2d)  :488-495
+                     (OpenCV 3.4.2 bilateralFilter_8u, non-IPP, fp32; parity unpinned)
 
 Parity status: the level logic and the marker allocation are in-tree Java (pinned by reading
 it: the known-answer tests in tests/test_nc.py are derived by hand from those lines); the gray
@@ -228,14 +230,91 @@ def markers(gray_img, lut):
     return lut[np.asarray(gray_img)].astype(np.int32)
 
 
-def marker_stage(bgr, depth, gisto_diap=False, multi_otsu_opt=False, median_blur=0):
+def _reflect101(p, n):
+    """borderInterpolate(p, n, BORDER_REFLECT_101), the loop form (borders wider than the
+    frame fold again)."""
+    if 0 <= p < n:
+        return p
+    if n == 1:
+        return 0
+    while not 0 <= p < n:
+        p = -p if p < 0 else 2 * n - 2 - p
+    return p
+
+
+def bilateral_tables(d):
+    """bilateralFilter_8u's set-up for bilateralFilter(srcGray, dst, d, 2d, 2d) (the BILATERIAL
+    branch, PictureService.java:488-490; OpenCV 3.4.2 imgproc bilateralFilter_8u): sigmas <= 0
+    become 1, radius = d / 2 (d <= 0: cvRound(1.5 sigma_space)), at least 1; the colour table
+    (float)exp(i*i*c) and the disc of taps (dy, dx, (float)exp(r*r*s)) with r = sqrt(dy^2 + dx^2)
+    <= radius, row-major.  Returns (radius, colour weights f32[256], [(dy, dx, f32 weight)])."""
+    import math
+
+    sc = ss = float(2 * int(d))
+    if sc <= 0:
+        sc = ss = 1.0
+    gcc = -0.5 / (sc * sc)
+    gsc = -0.5 / (ss * ss)
+    radius = int(d) // 2 if d > 0 else int(np.rint(ss * 1.5))
+    radius = max(radius, 1)
+    cw = np.array([np.float32(math.exp((i * i) * gcc)) for i in range(256)], np.float32)
+    taps = []
+    for i in range(-radius, radius + 1):
+        for j in range(-radius, radius + 1):
+            r = math.sqrt(float(i) * i + float(j) * j)
+            if r > radius:
+                continue
+            taps.append((i, j, np.float32(math.exp(r * r * gsc))))
+    return radius, cw, taps
+
+
+def bilateral(g, d):
+    """bilateralFilter(srcGray, dst, d, 2d, 2d) on an 8-bit gray plane, BORDER_REFLECT_101, in
+    fp32 as OpenCV 3.4.2's non-IPP x86 path computes it: taps in groups of four, each group's
+    weights w = colour[|v - v0|] * space and products w * v summed pairwise ((0+1)+(2+3), the
+    SSE3 horizontal adds) into the running sums, the last maxk % 4 taps added one at a time;
+    dst = cvRound(sum / wsum).  Parity unpinned: an IPP-enabled OpenCV runs IPP's own filter."""
+    g = np.asarray(g, np.uint8)
+    H, W = g.shape
+    radius, cw, taps = bilateral_tables(d)
+    if H == 0 or W == 0:
+        return g.copy()
+    rows = np.array([_reflect101(p, H) for p in range(-radius, H + radius)])
+    cols = np.array([_reflect101(p, W) for p in range(-radius, W + radius)])
+    pad = g[np.ix_(rows, cols)].astype(np.int32)
+    v0 = g.astype(np.int32)
+
+    def tap(k):
+        dy, dx, sw = taps[k]
+        v = pad[radius + dy:radius + dy + H, radius + dx:radius + dx + W]
+        w = cw[np.abs(v - v0)] * sw
+        return w, w * v.astype(np.float32)
+
+    s = np.zeros((H, W), np.float32)
+    ws = np.zeros((H, W), np.float32)
+    n4 = len(taps) // 4 * 4
+    for k in range(0, n4, 4):
+        (w0, p0), (w1, p1), (w2, p2), (w3, p3) = (tap(k + i) for i in range(4))
+        ws = ws + ((w0 + w1) + (w2 + w3))
+        s = s + ((p0 + p1) + (p2 + p3))
+    for k in range(n4, len(taps)):
+        w, p = tap(k)
+        s = s + p
+        ws = ws + w
+    return np.rint(s / ws).astype(np.uint8)
+
+
+def marker_stage(bgr, depth, gisto_diap=False, multi_otsu_opt=False, median_blur=0, bilateral_d=None):
     """gray, hist, levels, markers of one BGR frame.  median_blur = k > 0: the MEDIAN_BLUR branch
     (PictureService.java:481-483), medianBlur(srcGray, k) before the histogram (restated as the
-    exact k x k median with replicated borders, oracle/shape_oracle.median)."""
+    exact k x k median with replicated borders, oracle/shape_oracle.median); else bilateral_d = d
+    (not None): the BILATERIAL branch (:488-495), bilateral(srcGray, d)."""
     g = gray(bgr)
     if median_blur:
         from oracle import shape_oracle
         g = shape_oracle.median(g, int(median_blur))
+    elif bilateral_d is not None:
+        g = bilateral(g, int(bilateral_d))
     h = hist256(g)
     lv = levels(h, bgr.shape[0], bgr.shape[1], depth, gisto_diap, multi_otsu_opt)
     return g, h, lv, markers(g, marker_lut(lv, gisto_diap))

@@ -112,6 +112,50 @@ def test_marker_stage_median_blur_even_mask(seg):
     assert e.value.code == _lib.MSG_EINVAL
 
 
+@pytest.mark.parametrize("d", [0, 1, 3, 5, 8, 15])
+@pytest.mark.parametrize("kind,shape", [("mosaic_noise", (211, 307)), ("random", (64, 96)), ("mosaic", (5, 7))])
+def test_marker_stage_bilateral(seg, d, kind, shape):
+    """BILATERIAL (PictureService.java:488-495): bilateralFilter(srcGray, dst, d, 2d, 2d), then
+    histogram, levels and markers from dst; bit-exact against oracle/nc_oracle.bilateral (fp32,
+    the same summation order; d = 0 is radius cvRound(1.5), the 5x7 frame folds its border
+    twice at d = 15)."""
+    torch = _torch()
+    img, _, _ = synth.frame(kind, shape[0], shape[1], 9)
+    g, h, lv, mk = O.marker_stage(img, 4, bilateral_d=d)
+    m = torch.empty(shape, dtype=torch.int32, device="cuda:0")
+    gray = torch.empty(shape, dtype=torch.uint8, device="cuda:0")
+    try:
+        got = seg.nc_marker_stage_dev(_dev(img), 4, m, _lib.MSG_NC_BILATERAL | _lib.MSG_NC_MASK(d), gray=gray)
+    except msegment.MsegError as e:  # a filtered frame with no level: the reference throws too
+        assert e.code == _lib.MSG_ESTATE and not lv
+        return
+    torch.cuda.synchronize()
+    assert np.array_equal(gray.cpu().numpy(), g)
+    assert got == lv
+    assert np.array_equal(m.cpu().numpy(), mk)
+
+
+def test_bilateral_1024_and_median_precedence(seg):
+    """A 1024^2 noisy mosaic through the BILATERIAL branch (d = 9: a 69-tap disc) bit-exact, and
+    MEDIAN_BLUR winning when both flags are set (the reference's if / else-if)."""
+    torch = _torch()
+    img = synth.mosaic_image(1024, 1024, 4, noise=3)
+    g, h, lv, mk = O.marker_stage(img, 4, bilateral_d=9)
+    assert not np.array_equal(g, O.gray(img))
+    m = torch.empty((1024, 1024), dtype=torch.int32, device="cuda:0")
+    gray = torch.empty((1024, 1024), dtype=torch.uint8, device="cuda:0")
+    assert seg.nc_marker_stage_dev(_dev(img), 4, m, _lib.MSG_NC_BILATERAL | _lib.MSG_NC_MASK(9), gray=gray) == lv
+    torch.cuda.synchronize()
+    assert np.array_equal(gray.cpu().numpy(), g)
+    assert np.array_equal(m.cpu().numpy(), mk)
+    g2, _, lv2, mk2 = O.marker_stage(img[:256, :256], 4, median_blur=5)
+    m2 = torch.empty((256, 256), dtype=torch.int32, device="cuda:0")
+    both = _lib.MSG_NC_MEDIAN_BLUR | _lib.MSG_NC_BILATERAL | _lib.MSG_NC_MASK(5)
+    assert seg.nc_marker_stage_dev(_dev(img[:256, :256]), 4, m2, both) == lv2
+    torch.cuda.synchronize()
+    assert np.array_equal(m2.cpu().numpy(), mk2)
+
+
 def test_marker_stage_multi_otsu(seg):
     torch = _torch()
     # three flat patches -> three flex levels -> the multi-Otsu override (k = 3)
@@ -144,7 +188,8 @@ def _oracle_nc(img, depth, opts, seed, mask=3):
     """notConnectedMarkers end to end on the CPU oracles, with the reference's Random draws."""
     gisto, otsu, colored = "GISTO_DIAP" in opts, "MULTI_OTSU" in opts, "COLORED" in opts
     g, h, lv, mk = O.marker_stage(img, depth, gisto_diap=gisto, multi_otsu_opt=otsu,
-                                  median_blur=mask if "MEDIAN_BLUR" in opts else 0)
+                                  median_blur=mask if "MEDIAN_BLUR" in opts else 0,
+                                  bilateral_d=mask if "BILATERIAL" in opts else None)
     n = len(lv)
     rnd = JavaRandom(seed)
     draw = lambda: [rnd.next_int(156) + 100 for _ in range(3)]  # noqa: E731
@@ -156,7 +201,8 @@ def _oracle_nc(img, depth, opts, seed, mask=3):
 
 
 @pytest.mark.parametrize("opts", [("COLORED",), ("COLORED", "GISTO_DIAP"), (), ("MEDIAN_BLUR", "COLORED"),
-                                  ("MEDIAN_BLUR", "BILATERIAL")])
+                                  ("MEDIAN_BLUR", "BILATERIAL"),
+                                  ("BILATERIAL",), ("BILATERIAL", "GISTO_DIAP", "COLORED")])
 def test_not_connected_markers_pipeline(opts):
     img, _, _ = synth.frame("mosaic_noise", 192, 160, 11)
     ps = msegment.PictureService(seed=2024)
@@ -204,10 +250,3 @@ def test_host_buffer_marker_stage(seg):
     with pytest.raises(msegment.MsegError) as e:
         seg.nc_marker_stage(np.full((4, 4, 3), 255, np.uint8), 3)
     assert e.value.code == _lib.MSG_ESTATE
-
-
-def test_not_connected_markers_bilateral_rejected():
-    img, _, _ = synth.frame("mosaic_noise", 32, 32, 11)
-    with pytest.raises(msegment.MsegError) as e:
-        msegment.PictureService(seed=1).not_connected_markers(img, 4, ("BILATERIAL",))
-    assert e.value.code == _lib.MSG_EINVAL

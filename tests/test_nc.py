@@ -157,3 +157,74 @@ def test_library_multi_otsu_matches_oracle_random():
         assert got == want
         for opt in (0, GISTO):
             assert np.array_equal(msegment.nc_marker_lut(got, opt), O.marker_lut(want, bool(opt)))
+
+
+def _bilateral_scalar(g, d):
+    """Pixel-by-pixel restatement of bilateralFilter_8u (one channel) with fp32 scalars and
+    OpenCV's borderInterpolate loop, written independently of the vectorised oracle."""
+    import math
+
+    f = np.float32
+    H, W = g.shape
+    sigma = 2.0 * d if d > 0 else 1.0
+    r = d // 2 if d > 0 else int(round(1.5 * sigma))
+    r = max(r, 1)
+    cw = [f(math.exp(i * i * (-0.5 / (sigma * sigma)))) for i in range(256)]
+    taps = [(i, j, f(math.exp(math.sqrt(i * i + j * j) ** 2 * (-0.5 / (sigma * sigma)))))
+            for i in range(-r, r + 1) for j in range(-r, r + 1) if math.sqrt(i * i + j * j) <= r]
+
+    def refl(p, n):
+        while n > 1 and not 0 <= p < n:
+            p = -p if p < 0 else 2 * n - 2 - p
+        return 0 if n == 1 else p
+
+    out = np.empty_like(g)
+    for y in range(H):
+        for x in range(W):
+            v0 = int(g[y, x])
+            ws = []
+            for dy, dx, sw in taps:
+                v = int(g[refl(y + dy, H), refl(x + dx, W)])
+                w = f(cw[abs(v - v0)] * sw)
+                ws.append((w, f(w * f(v))))
+            s = f(0)
+            t = f(0)
+            n4 = len(ws) // 4 * 4
+            for k in range(0, n4, 4):
+                (w0, p0), (w1, p1), (w2, p2), (w3, p3) = ws[k:k + 4]
+                t = f(t + f(f(w0 + w1) + f(w2 + w3)))
+                s = f(s + f(f(p0 + p1) + f(p2 + p3)))
+            for w, p in ws[n4:]:
+                s = f(s + p)
+                t = f(t + w)
+            out[y, x] = int(np.rint(f(s / t)))
+    return out
+
+
+@pytest.mark.parametrize("d", [0, 1, 2, 3, 5, 8, 13])
+def test_oracle_bilateral_matches_scalar_restatement(d):
+    """The BILATERIAL pre-filter (PictureService.java:488-495): the vectorised oracle against a
+    pixel loop, on noise (every tap weight in play) and on a frame smaller than the disc."""
+    rng = np.random.default_rng(d)
+    for shape in ((9, 13), (3, 2), (1, 5)):
+        g = rng.integers(0, 256, shape, dtype=np.uint8)
+        assert np.array_equal(O.bilateral(g, d), _bilateral_scalar(g, d)), shape
+
+
+def test_oracle_bilateral_known_answers():
+    # a flat plane is a fixed point; a step edge keeps its sides (colour weights at distance 200
+    # are exp(-200^2 / 50) ~ 0); d <= 0 gives radius cvRound(1.5) = 2, a 13-tap disc
+    assert np.array_equal(O.bilateral(np.full((6, 7), 93, np.uint8), 5), np.full((6, 7), 93, np.uint8))
+    step = np.zeros((8, 8), np.uint8)
+    step[:, 4:] = 200
+    assert np.array_equal(O.bilateral(step, 5), step)
+    radius, cw, taps = O.bilateral_tables(0)
+    assert radius == 2 and len(taps) == 13 and cw[0] == 1.0
+    radius, cw, taps = O.bilateral_tables(5)
+    assert radius == 2 and len(taps) == 13 and cw.dtype == np.float32
+    assert O.bilateral_tables(9)[0] == 4 and len(O.bilateral_tables(9)[2]) == 49
+    # one bright pixel among dark ones is pulled only slightly (colour weight exp(-100^2/200))
+    g = np.full((5, 5), 10, np.uint8)
+    g[2, 2] = 110
+    out = O.bilateral(g, 3)
+    assert out[2, 2] == 110 and out[0, 0] == 10
