@@ -21,6 +21,11 @@
  * MSG_EINVAL mirrors cv::watershed's CV_Assert (type/size/stride checks); the JNI shim
  *  turns any nonzero code into a Java exception like CvException.
  *
+ * Frame sizes: the flood entry points (watershed, colorize, edge weights) take frames up to
+ * about 2^29 pixels (4 rows*cols + 16 and the frame's 4x4-tile padded size below 2^31 - 512:
+ * e.g. 23168 x 23168 or 16387 x 32749); the marker stages (msg_nc_*, msg_shape_*,
+ * msg_color_*) take up to 2^28.  Larger frames are MSG_EINVAL.
+ *
  * Threading: a context is used by one thread at a time; contexts are independent.
  */
 #ifndef MSEGMENT_H

@@ -319,10 +319,27 @@ int ensure_stage(msg_ctx* c, long long N) {
   return MSG_OK;
 }
 
-int check_size(msg_ctx* c, int rows, int cols) {
+// Frame-size limits.  The flood indexes its tiled state (4x4 tiles plus a tile row of margin
+// either side) and its bucket FIFOs (up to 4 slots per pixel; slot s is stored as the state
+// -3 - s, which must stay clear of the phase-1 states 0x80000000 | level) with 32-bit ints, so
+// 4N + 16 and the padded tiled count stay below 2^31 - 512: frames up to ~2^29 pixels
+// (23168^2, 16384 x 32767).  Byte offsets of the BGR frame (3N < 1.61e9) fit signed 32 bits
+// there too.  The marker stages are audited for 2^28 pixels only and keep that bound.
+constexpr long long kStageMaxPixels = 1ll << 28;
+constexpr long long kFloodIndexLimit = (1ll << 31) - 512;
+
+int check_size(msg_ctx* c, int rows, int cols, bool flood = false) {
   if (rows < 0 || cols < 0) return fail(c, MSG_EINVAL, "negative size %d x %d", rows, cols);
-  if ((long long)rows * cols > (1ll << 28))
-    return fail(c, MSG_EINVAL, "frame too large for one context: %d x %d", rows, cols);
+  const long long N = (long long)rows * cols;
+  if (!flood) {
+    if (N > kStageMaxPixels)
+      return fail(c, MSG_EINVAL, "frame too large for the marker stage: %d x %d (2^28 pixels at most)", rows, cols);
+    return MSG_OK;
+  }
+  const long long Np = (long long)((rows + 3) / 4) * ((cols + 3) / 4) * 16 + 2 * tile_margin(cols);
+  if (4 * N + 16 >= kFloodIndexLimit || Np >= kFloodIndexLimit)
+    return fail(c, MSG_EINVAL, "frame too large for the flood's 32-bit indices: %d x %d (about 2^29 pixels at most)",
+                rows, cols);
   return MSG_OK;
 }
 
@@ -902,7 +919,7 @@ int msg_get_kernel_profile(msg_ctx* c, msg_kernel_profile* out, int max_entries,
 int msg_watershed_dev(msg_ctx* c, const void* d_bgr, const void* d_markers_in, void* d_labels,
                       int rows, int cols, void* stream) {
   if (!c) return MSG_EINVAL;
-  int rc = check_size(c, rows, cols);
+  int rc = check_size(c, rows, cols, true);
   if (rc) return rc;
   if ((long long)rows * cols > 0 && (!d_bgr || !d_markers_in || !d_labels))
     return fail(c, MSG_EINVAL, "null device pointer");
@@ -917,7 +934,7 @@ int msg_watershed_dev(msg_ctx* c, const void* d_bgr, const void* d_markers_in, v
 int msg_colorize_dev(msg_ctx* c, const void* d_labels, int rows, int cols, int depth,
                      const void* d_palette_bgr, void* d_dst_bgr, void* d_gray, void* stream) {
   if (!c) return MSG_EINVAL;
-  int rc = check_size(c, rows, cols);
+  int rc = check_size(c, rows, cols, true);
   if (rc) return rc;
   if (depth < 0) return fail(c, MSG_EINVAL, "negative depth");
   if ((long long)rows * cols > 0 && (!d_labels || !d_dst_bgr))
@@ -935,7 +952,7 @@ int msg_watershed_colorize_dev(msg_ctx* c, const void* d_bgr, const void* d_mark
                                const void* d_palette_bgr, void* d_dst_bgr, void* d_gray,
                                void* stream) {
   if (!c) return MSG_EINVAL;
-  int rc = check_size(c, rows, cols);
+  int rc = check_size(c, rows, cols, true);
   if (rc) return rc;
   if (depth < 0) return fail(c, MSG_EINVAL, "negative depth");
   if ((long long)rows * cols > 0 && (!d_bgr || !d_markers_in || !d_labels || !d_dst_bgr))
@@ -952,7 +969,7 @@ int msg_watershed_colorize_dev(msg_ctx* c, const void* d_bgr, const void* d_mark
 int msg_edge_weights_dev(msg_ctx* c, const void* d_bgr, void* d_wright, void* d_wdown, int rows,
                          int cols, void* stream) {
   if (!c) return MSG_EINVAL;
-  int rc = check_size(c, rows, cols);
+  int rc = check_size(c, rows, cols, true);
   if (rc) return rc;
   const long long N = (long long)rows * cols;
   if (N == 0) return MSG_OK;
@@ -984,9 +1001,9 @@ int msg_edge_weights_dev(msg_ctx* c, const void* d_bgr, void* d_wright, void* d_
 }
 
 static int host_args(msg_ctx* c, const void* bgr, size_t bgr_stride, const void* markers,
-                     size_t marker_stride, int rows, int cols) {
+                     size_t marker_stride, int rows, int cols, bool flood = false) {
   if (!c) return MSG_EINVAL;
-  int rc = check_size(c, rows, cols);
+  int rc = check_size(c, rows, cols, flood);
   if (rc) return rc;
   if ((long long)rows * cols == 0) return MSG_OK;
   if (!bgr || !markers) return fail(c, MSG_EINVAL, "null host pointer");
@@ -1000,7 +1017,7 @@ int msg_watershed_colorize(msg_ctx* c, const uint8_t* bgr, size_t bgr_stride, in
                            size_t marker_stride, int rows, int cols, int depth,
                            const uint8_t* palette_bgr, uint8_t* dst_bgr, size_t dst_stride,
                            uint8_t* gray, size_t gray_stride) {
-  int rc = host_args(c, bgr, bgr_stride, markers, marker_stride, rows, cols);
+  int rc = host_args(c, bgr, bgr_stride, markers, marker_stride, rows, cols, true);
   if (rc) return rc;
   const long long N = (long long)rows * cols;
   if (N == 0) return MSG_OK;
@@ -1054,7 +1071,7 @@ int msg_watershed(msg_ctx* c, const uint8_t* bgr, size_t bgr_stride, int32_t* ma
 int msg_colorize(msg_ctx* c, const int32_t* labels, size_t label_stride, int rows, int cols,
                  int depth, const uint8_t* palette_bgr, uint8_t* dst_bgr, size_t dst_stride) {
   if (!c) return MSG_EINVAL;
-  int rc = check_size(c, rows, cols);
+  int rc = check_size(c, rows, cols, true);
   if (rc) return rc;
   const long long N = (long long)rows * cols;
   if (N == 0) return MSG_OK;

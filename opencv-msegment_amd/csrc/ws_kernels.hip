@@ -72,7 +72,7 @@ __device__ __forceinline__ void st_granule(unsigned long long* p, unsigned long 
 // channel differences and 2 maxima per pixel), so every channel byte is extracted once per row
 // and each |a - b| is one v_sad_u16 (operands < 2^16): 16.5 -> ~10 VALU ops per pixel, which
 // took the 4096^2 launch from 18.1 to 14.7 us (R = 1; scripts/exp/stream_variants.hip).  Frames
-// are <= 2^28 pixels (check_size), so 32-bit offsets suffice.
+// are < 2^29 pixels (check_size), so 32-bit offsets suffice (3N < 2^31).
 // k_edge_weights: any shape, 4 pixels per thread.
 __device__ __forceinline__ uint32_t absdiff(uint32_t x, uint32_t y) { return __builtin_amdgcn_sad_u16(x, y, 0u); }
 __device__ __forceinline__ uint32_t linf_ch(const uint32_t* p, const uint32_t* q) {
@@ -186,7 +186,7 @@ constexpr int PREP_LDW = RSEG + 5;                   // LDS row stride (words): 
 constexpr int PREP_RAW = (3 * PREP_COLS + 8) / 4 + 1;  // dwords of one BGR row segment
 
 // thread = one tile row (4 pixels): tile tid >> 2, row tid & 3, so 4 consecutive lanes write one
-// whole 128-B tile line; frames are <= 2^28 pixels, so 32-bit offsets (3N < 2^30) suffice.
+// whole 128-B tile line; frames are < 2^29 pixels, so 32-bit offsets (3N < 2^31) suffice.
 __global__ __launch_bounds__(RSEG) void k_prep(Ws ws, const int32_t* __restrict__ mk_in) {
   static_assert(RSEG >= NQ && RSEG % 64 == 0 && PREP_RAW <= RSEG, "strip = RSEG/4 tiles x 4 rows = RSEG threads");
   __shared__ unsigned caph[NQ];
@@ -984,7 +984,7 @@ __device__ __forceinline__ int fold_lab(int lab, int v) {
 
 
 struct Item {
-  int p;             // tiled pixel index (frames <= 2^28 pixels)
+  int p;             // tiled pixel index (< 2^31 - 512: check_size)
   int base_lab;      // fold of the settled (>0) neighbours: 0, a label, or WSHED
   unsigned zero_mask;
   unsigned wts;      // 4 packed 8-bit edge weights, directions L,R,T,B
@@ -2379,7 +2379,7 @@ __global__ __launch_bounds__(256) void k_leftover_diag(Ws ws, long long nt, unsi
     const int s = ws.mk[t];
     if (s > -3) continue;
     atomicAdd(out + 3, 1ull);
-    if (s < -3 - (1 << 29)) {
+    if (is_p1(s)) {
       atomicAdd(out + 0, 1ull);
       continue;
     }
@@ -2415,7 +2415,7 @@ __global__ __launch_bounds__(256) void k_untile(const int32_t* __restrict__ mk, 
   // whole tiles), and the 16 lanes of one tile row of a wave store 256 B of labels, 192 B of
   // colours and 64 B of gray, each one 16-B / 12-B / 4-B store per lane (the 8-B unit layout it
   // replaces stored colours as three 2-B pieces: 33.5 -> 28.3 us at 4096^2 in
-  // scripts/exp/stream_variants.hip).  Frames are <= 2^28 pixels: 32-bit tile arithmetic.
+  // scripts/exp/stream_variants.hip).  Frames are < 2^29 pixels: 32-bit tile arithmetic.
   extern __shared__ __attribute__((aligned(16))) uint32_t spal[];
   const bool lds_pal = dst != nullptr && pal != nullptr && depth <= PAL_LDS_MAX;
   if (lds_pal) {

@@ -12,7 +12,8 @@ constexpr int SUB = CH / BS;     // sub-rounds per chunk
 constexpr int WSHED = -1;        // cv::watershed WSHED
 constexpr int INQ = -2;          // cv::watershed IN_QUEUE, before the pixel has a queue slot
 // A queued pixel's state word also carries its queue slot (one random load instead of two):
-// state = -3 - slot  (<= -3).  Slots are < 2^31 - 8 (frames are limited to 2^29 pixels).
+// state = -3 - slot  (<= -3).  Slots are < 4N + 16 < 2^31 - 512 (check_size), clear of the
+// phase-1 states 0x80000000 | level.
 __host__ __device__ inline int queued_state(int slot) { return -3 - slot; }
 __host__ __device__ inline int state_slot(int state) { return -3 - state; }
 constexpr int NONE = 0x7fffffff;

@@ -110,11 +110,13 @@ def main():
 
 # (kind, H, W, seed): SURVEY.md §8d seeds -- cfg2 1024^2 s=1, cfg3 4096^2 s=2, cfg4 16384^2 s=3,
 # cfg5's first frame 4096^2 s=100; plus a large frame with ragged 4x4 tiles in both directions;
-# cfg3's stress variants (mosaic+noise and uniform-random at 4096^2 s=2)
+# cfg3's stress variants (mosaic+noise and uniform-random at 4096^2 s=2);
+# a 537 M-pixel frame (2x config 4) near the flood's 32-bit index limit
 DIGEST_CASES = [("mosaic", 1024, 1024, 1), ("mosaic_noise", 1024, 1024, 1),
                 ("random", 512, 512, 3), ("mosaic", 4096, 4096, 2), ("mosaic", 16384, 16384, 3),
                 ("mosaic", 4096, 4096, 100), ("mosaic", 3001, 5003, 7),
-                ("mosaic_noise", 4096, 4096, 2), ("random", 4096, 4096, 2)]
+                ("mosaic_noise", 4096, 4096, 2), ("random", 4096, 4096, 2),
+                ("mosaic", 16387, 32749, 11)]  # above 2^28 pixels, ragged tiles: the flood's size limit
 
 
 def write_digests(only=None):

@@ -142,6 +142,30 @@ def test_config4_16384_mosaic_digest_single_gpu(seg):
     assert int((out == -1).sum()) == dg["wshed_pixels"]
 
 
+def test_frame_above_2_28_pixels_digest(seg):
+    """16387 x 32749 = 537 M pixels (2x config 4, ragged 4x4 tiles in both directions): above
+    round 1's 2^28-pixel limit and just below the flood's 32-bit index limit (4N + 16 queue slots,
+    check_size), against the oracle's digest (tests/golden/make_golden.py)."""
+    import torch
+
+    dg = json.load(open(os.path.join(GOLD, "digests.json")))["mosaic_16387x32749_s11"]
+    img, m, d = synth.frame("mosaic", 16387, 32749, 11)
+    assert hashlib.sha256(m.tobytes()).hexdigest() == dg["markers_sha256"]
+    dev = torch.device("cuda", seg.device)
+    t_img = torch.from_numpy(img).to(dev)
+    del img
+    t_m = torch.from_numpy(m).to(dev)
+    del m
+    seg.watershed_dev(t_img, t_m, t_m)
+    torch.cuda.synchronize(dev)
+    del t_img
+    out = t_m.cpu().numpy()
+    del t_m
+    torch.cuda.empty_cache()
+    assert hashlib.sha256(out.tobytes()).hexdigest() == dg["labels_sha256"]
+    assert int((out == -1).sum()) == dg["wshed_pixels"]
+
+
 def test_large_ragged_mosaic_digest(seg):
     """3001 x 5003: ragged 4x4 tiles in both directions (3001 % 4 == 1, 5003 % 4 == 3) at 15 M
     pixels, against the oracle's digest, plus the invariants."""
@@ -367,7 +391,8 @@ def test_c_abi_error_paths(seg):
     mp = mk.ctypes.data_as(ctypes.c_void_p)
     bad = [
         lambda: L.msg_watershed(h, ip, 24, mp, 32, -1, 8),          # negative rows
-        lambda: L.msg_watershed(h, ip, 24, mp, 32, 1 << 15, 1 << 14),  # > 2^28 pixels
+        lambda: L.msg_watershed(h, ip, 24, mp, 32, 1 << 15, 1 << 14),  # 2^29 pixels: 4N slots overflow
+        lambda: L.msg_watershed(h, ip, 24, mp, 32, 1, (1 << 29) - 1024),  # 1-row frame: 4x4 tile padding overflows
         lambda: L.msg_watershed(h, None, 24, mp, 32, 8, 8),         # null image
         lambda: L.msg_watershed(h, ip, 23, mp, 32, 8, 8),           # bgr stride < 3 cols
         lambda: L.msg_watershed(h, ip, 24, mp, 30, 8, 8),           # marker stride not 4-aligned
@@ -378,6 +403,8 @@ def test_c_abi_error_paths(seg):
     for k, call in enumerate(bad):
         assert call() == _lib.MSG_EINVAL, k
         assert L.msg_last_error(h), k
+        if k in (1, 2):
+            assert b"32-bit indices" in L.msg_last_error(h), k
     out = mk.copy()
     assert L.msg_watershed(h, ip, 24, out.ctypes.data_as(ctypes.c_void_p), 32, 8, 8) == 0
     assert np.array_equal(out, ws_oracle.watershed(img, mk))
