@@ -72,7 +72,7 @@ class BrightLevel(ctypes.Structure):
     _fields_ = [("start", ctypes.c_int32), ("end", ctypes.c_int32), ("count", ctypes.c_int32)]
 
 
-NKERNELS = 21
+NKERNELS = 22  # MSG_NKERNELS (include/msegment.h; tests/test_abi.py checks the two agree)
 
 
 def build(arch="gfx950"):

@@ -38,3 +38,19 @@ def test_null_context_is_rejected_without_gpu():
     L = _lib.load()
     assert L.msg_watershed(None, None, 0, None, 0, 4, 4) == _lib.MSG_EINVAL
     assert L.msg_create(None, 0, 0) == _lib.MSG_EINVAL
+
+
+def test_python_constants_match_header():
+    """The ctypes mirror's constants (msegment/_lib.py) equal include/msegment.h's #defines: a
+    stale NKERNELS would cut the kernel profile short, a stale option bit would select the wrong
+    pre-filter."""
+    import re
+
+    from msegment import _lib
+
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "msegment.h")).read()
+    defs = dict(re.findall(r"#define (MSG_\w+)\s+\(?(-?(?:0x)?[0-9a-fA-F]+)u?\)?", hdr))
+    assert int(defs["MSG_NKERNELS"], 0) == _lib.NKERNELS
+    for name in ("MSG_OK", "MSG_EINVAL", "MSG_EHIP", "MSG_ENOMEM", "MSG_ETIMEOUT", "MSG_ESTATE", "MSG_ERANGE",
+                 "MSG_NC_GISTO_DIAP", "MSG_NC_MULTI_OTSU", "MSG_NC_MEDIAN_BLUR", "MSG_NC_BILATERAL"):
+        assert int(defs[name], 0) == getattr(_lib, name), name
