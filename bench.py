@@ -649,7 +649,8 @@ def main(argv=None):
                                       else ("colorAutoMarkerWatershed marker stage (depth %d) + watershed of "
                                             "the sharpened frame" % color_depth[0]) if COLOR
                                       else "watershed",
-                                      ({1024: "2", 16384: "4 frame on one GPU"}.get(S, "3") if K == 1
+                                      ({1024: "2", 4096: "3", 16384: "4 frame on one GPU"}.get(
+                                          S, "-: a %d-pixel frame" % (S * S)) if K == 1
                                        else "5 batching") if world == 1 else "5"),
                        "frames_per_rank_per_step": K, "parallelism": "replicas%d (no collectives)" % world},
             "roofline": roof,
