@@ -27,6 +27,27 @@ ShapeResult = namedtuple("ShapeResult", "dst bw labels depth")
 ColorResult = namedtuple("ColorResult", "dst bw labels depth sharp")
 
 
+def nc_option_flags(options, filter_mask_size):
+    """msg_nc_marker_stage option bits for notConnectedMarkers' AlgorithmOptions
+    (PictureService.java:469-495): GISTO_DIAP, MULTI_OTSU, and one pre-filter -- MEDIAN_BLUR wins
+    over BILATERIAL (the reference's if / else-if) -- with filterMaskSize in bits 8-15.  For
+    BILATERIAL every size <= 0 behaves as 0 in bilateralFilter (sigma <= 0 -> 1, radius
+    cvRound(1.5)), so it is passed as 0; sizes above 255 do not fit the option bits (MsegError)."""
+    from . import MsegError, _lib
+
+    opts = set(options)
+    flags = (_lib.MSG_NC_GISTO_DIAP if "GISTO_DIAP" in opts else 0) | (
+        _lib.MSG_NC_MULTI_OTSU if "MULTI_OTSU" in opts else 0)
+    k = int(filter_mask_size)
+    if "MEDIAN_BLUR" in opts:
+        flags |= _lib.MSG_NC_MEDIAN_BLUR | _lib.MSG_NC_MASK(k)
+    elif "BILATERIAL" in opts:
+        if k > 255:
+            raise MsegError(_lib.MSG_EINVAL, "BILATERIAL mask size %d: at most 255" % k)
+        flags |= _lib.MSG_NC_BILATERAL | _lib.MSG_NC_MASK(max(k, 0))
+    return flags
+
+
 class PictureService:
     def __init__(self, segmenter=None, seed=None, device=0):
         from . import Segmenter
@@ -84,17 +105,8 @@ class PictureService:
         import numpy as np
         import torch
 
-        from . import MsegError, _lib
-
         opts = set(options)
-        flags = (_lib.MSG_NC_GISTO_DIAP if "GISTO_DIAP" in opts else 0) | (
-            _lib.MSG_NC_MULTI_OTSU if "MULTI_OTSU" in opts else 0)
-        if "MEDIAN_BLUR" in opts:  # MEDIAN_BLUR wins (if / else if, :481 / :488)
-            flags |= _lib.MSG_NC_MEDIAN_BLUR | _lib.MSG_NC_MASK(filter_mask_size)
-        elif "BILATERIAL" in opts:
-            if not 0 <= int(filter_mask_size) <= 255:
-                raise MsegError(_lib.MSG_EINVAL, "BILATERIAL mask size %d: 0..255" % filter_mask_size)
-            flags |= _lib.MSG_NC_BILATERAL | _lib.MSG_NC_MASK(filter_mask_size)
+        flags = nc_option_flags(opts, filter_mask_size)
         colored = "COLORED" in opts
         src = np.ascontiguousarray(np.asarray(src, dtype=np.uint8))
         H, W = src.shape[:2]

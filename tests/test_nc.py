@@ -228,3 +228,19 @@ def test_oracle_bilateral_known_answers():
     g[2, 2] = 110
     out = O.bilateral(g, 3)
     assert out[2, 2] == 110 and out[0, 0] == 10
+
+
+def test_nc_option_flags():
+    """AlgorithmOptions -> msg_nc_marker_stage bits (PictureService.java:469-495): MEDIAN_BLUR wins
+    over BILATERIAL (if / else-if), the mask size rides in bits 8-15, a BILATERIAL size <= 0 acts
+    as 0 (bilateralFilter: sigma <= 0 -> 1, radius 2), one above 255 is rejected."""
+    from msegment.picture_service import nc_option_flags
+
+    assert nc_option_flags((), 3) == 0
+    assert nc_option_flags(("GISTO_DIAP", "MULTI_OTSU", "COLORED"), 3) == _lib.MSG_NC_GISTO_DIAP | OTSU
+    assert nc_option_flags(("MEDIAN_BLUR", "BILATERIAL"), 5) == _lib.MSG_NC_MEDIAN_BLUR | _lib.MSG_NC_MASK(5)
+    assert nc_option_flags(("BILATERIAL",), 9) == _lib.MSG_NC_BILATERAL | (9 << 8)
+    assert nc_option_flags(("BILATERIAL",), -4) == _lib.MSG_NC_BILATERAL
+    assert np.array_equal(O.bilateral_tables(-4)[2], O.bilateral_tables(0)[2])
+    with pytest.raises(msegment.MsegError):
+        nc_option_flags(("BILATERIAL",), 256)
