@@ -264,7 +264,8 @@ int msg_shape_markers(msg_ctx* ctx, const uint8_t* bgr, size_t bgr_stride, int r
 
 /* ---- COLOR_METHOD marker stage: the caller that builds the flood's seeds in
  * PictureService.colorAutoMarkerWatershed (PictureService.java:301-392):
- *   white -> black, src - filter2D(9x1 Laplacian column) saturated = the flood's src (:308-333)
+ *   src - filter2D(9x1 Laplacian column) saturated = the flood's src (:323-333; the white -> black
+ *   loop :309-318 never fires in Java: PixelUtil.java:19 compares a signed byte with 255)
  *   -> bw = threshold(BGR2GRAY, OTSU) (:338, :938-943)
  *   -> distanceTransform(bw, DIST_L2, 5), normalize(NORM_MINMAX) (:343, :1018-1023)
  *   -> threshold(0.4), dilate 3x3 (:348-350)

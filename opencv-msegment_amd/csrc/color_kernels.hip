@@ -1,7 +1,9 @@
 // color_kernels.hip -- gfx950 kernels of the COLOR_METHOD marker stage, the caller that builds the
 // flood's seeds in PictureService.colorAutoMarkerWatershed (PictureService.java:301-366):
 //
-//   white -> black, src - filter2D(9x1 Laplacian), saturate      :308-333   k_cm_sharpen
+//   src - filter2D(9x1 Laplacian), saturate                      :308-333   k_cm_sharpen
+//     (the white -> black loop at :309-318 never fires: PixelUtil.checkPixelRGB, PixelUtil.java:19,
+//      compares Java's signed byte -- 0xFF reads -1 -- with int 255, so white stays white)
 //   bw = BGR2GRAY + threshold(OTSU)                              :338, :938 k_gray_hist + host Otsu
 //   distanceTransform(bw, DIST_L2, 5)                            :343, :1020 k_cm_dt_init, k_cm_dt_sweep
 //   normalize(NORM_MINMAX), threshold(0.4), dilate(3x3)          :1021, :348-350 k_cm_minmax, k_cm_peaks, k_cm_dilate3
@@ -28,8 +30,9 @@ __device__ __forceinline__ int cm_reflect101(int p, int n) {
   return p;
 }
 
-// res(y, x, c) = clamp(9 s(y) - sum_{0 < |k| <= 4} s(reflect101(y + k)), 0, 255), s = the pixel
-// with white (255, 255, 255) replaced by black.  One thread per pixel.
+// res(y, x, c) = clamp(9 s(y) - sum_{0 < |k| <= 4} s(reflect101(y + k)), 0, 255), s = the source
+// pixel as it is (the reference's white -> black loop is a no-op in Java, see the header).  One
+// thread per pixel.
 __global__ __launch_bounds__(256) void k_cm_sharpen(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ out,
                                                     int H, int W) {
   const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
@@ -39,8 +42,7 @@ __global__ __launch_bounds__(256) void k_cm_sharpen(const uint8_t* __restrict__ 
   for (int k = -4; k <= 4; ++k) {
     const int yy = cm_reflect101(y + k, H);
     const uint8_t* q = bgr + ((long long)yy * W + x) * 3;
-    int b = q[0], g = q[1], r = q[2];
-    if (b == 255 && g == 255 && r == 255) b = g = r = 0;
+    const int b = q[0], g = q[1], r = q[2];
     const int wgt = (k == 0) ? 9 : -1;
     acc0 += wgt * b;
     acc1 += wgt * g;

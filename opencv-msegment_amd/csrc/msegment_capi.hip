@@ -405,22 +405,29 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   ws.N = N;
   ws.qcap = c->qcap;
 
-  // speculative generations: tiled indices must fit their 28-bit log field
+  // speculative generations: tiled indices must fit their 28-bit log field.  The engine's
+  // workspace (~64 B/px) is allocated lazily: only once a flood of this context has entered the
+  // interrupt-dense (serial-pop) regime, which k_scan reports through the progress mirror; smooth
+  // frames never pay for it.  From then on it is kept (msg_set_speculative(ctx, 0) frees it).
   const long long ntiled = (long long)((H + 3) / 4) * ws.Wt * 16;
   const bool spec = c->spec && ntiled <= (1ll << 28) && H >= 3 && W >= 3;
-  ws.scl = nullptr; ws.sfin = nullptr; ws.slab = nullptr; ws.stl = nullptr; ws.slog = nullptr;
-  ws.srec = nullptr; ws.ssig = nullptr; ws.sfrec = nullptr; ws.stmp = nullptr; ws.sflag = nullptr;
-  ws.snp = 0;
-  ws.slogcap = 0;
-  if (spec) {
+  auto bind_spec = [&](bool on) {
+    ws.scl = on ? c->d_scl : nullptr; ws.sfin = on ? c->d_sfin : nullptr;
+    ws.slab = on ? c->d_slab : nullptr; ws.stl = on ? c->d_stl : nullptr;
+    ws.slog = on ? c->d_slog : nullptr; ws.srec = on ? c->d_srec : nullptr;
+    ws.ssig = on ? c->d_ssig : nullptr; ws.sfrec = on ? c->d_sfrec : nullptr;
+    ws.stmp = on ? c->d_stmp : nullptr; ws.sflag = on ? c->d_sflag : nullptr;
+    ws.snp = on ? c->spec_np : 0;
+    ws.slogcap = on ? c->spec_logcap : 0;
+    ws.spec_lazy = (spec && !on) ? 1 : 0;
+  };
+  bool spec_bound = false;
+  if (spec && c->spec_np > 0) {  // allocated by an earlier flood: (re)size and arm it now
     rc = ensure_spec(c, ntiled, N, st);
     if (rc) return rc;
-    ws.scl = c->d_scl; ws.sfin = c->d_sfin; ws.slab = c->d_slab; ws.stl = c->d_stl;
-    ws.slog = c->d_slog; ws.srec = c->d_srec; ws.ssig = c->d_ssig; ws.sfrec = c->d_sfrec;
-    ws.stmp = c->d_stmp; ws.sflag = c->d_sflag;
-    ws.snp = c->spec_np;
-    ws.slogcap = c->spec_logcap;
+    spec_bound = true;
   }
+  bind_spec(spec_bound);
   const int npx = (int)((N + CH - 1) / CH);
   const int gres = std::max(1, std::min(c->res_grid, (int)((N + RBS - 1) / RBS)));
   const int gsc = std::min(npx * (CH / 1024), 1024);
@@ -445,6 +452,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   // after queueing a group the host spins until the previous group's last iteration reported.
   __atomic_store_n(&c->h_mir[0], -1, __ATOMIC_RELEASE);
   c->h_mir[4] = 0;
+  c->h_mir[5] = 0;
   int it = 0, prev_end = -1;
   c->group = 4;
   long long syncs = 0;
@@ -455,7 +463,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   constexpr int SPEC_ITER_ROUNDS = 3;
   const int gflat = std::max(1, c->cus);
   for (;;) {
-    const bool spec_it = spec && c->h_mir[4] != 0;
+    const bool spec_it = spec_bound && c->h_mir[4] != 0;
     for (int g = 0; g < c->group; ++g, ++it) {
       if (spec_it) {
         for (int r = 0; r < SPEC_ITER_ROUNDS; ++r)
@@ -475,6 +483,15 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
       if (rc) return rc;
       ++syncs;
       if (c->h_mir[1] || c->h_mir[2]) break;
+      if (spec && !spec_bound && c->h_mir[5]) {
+        // first entry into the serial regime: allocate the engine; launches from here on carry it
+        // (the zero fills are stream-ordered after the iterations already queued, which run
+        // without it, and before the first launch that may use it)
+        rc = ensure_spec(c, ntiled, N, st);
+        if (rc) return rc;
+        spec_bound = true;
+        bind_spec(true);
+      }
       // fewer queued items -> fewer batches left: shrink the group so that the iterations
       // enqueued past the end of the flood (no-ops, but each still a launch) stay few
       const int rem = c->h_mir[3];
@@ -509,7 +526,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   c->stats.spec_executions = tail.spec.execs;
   c->stats.spec_cascade_pops = tail.spec.cpops;
   c->stats.spec_fallbacks = tail.spec.fallbacks;
-  if (spec) c->stag = tail.spec.T;
+  if (spec_bound) c->stag = tail.spec.T;
   c->epoch += (unsigned)std::min<long long>(tail.batches + 4, 0x7fffffff);
   if (tail.error & ERR_TIMEOUT)
     return fail(c, MSG_ETIMEOUT, "in-kernel wait timed out (grid not co-resident?)");
@@ -872,7 +889,11 @@ int msg_get_stats(const msg_ctx* c, msg_stats* out) {
 int msg_set_speculative(msg_ctx* c, int enable) {
   if (!c) return MSG_EINVAL;
   c->spec = enable != 0;
-  for (msg_ctx* sub : c->subs) sub->spec = c->spec;
+  if (!c->spec) free_spec(c);  // the engine's workspace comes back on its next first use
+  for (msg_ctx* sub : c->subs) {
+    sub->spec = c->spec;
+    if (!sub->spec) free_spec(sub);
+  }
   return MSG_OK;
 }
 

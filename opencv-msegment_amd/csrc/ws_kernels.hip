@@ -1679,6 +1679,7 @@ __global__ __launch_bounds__(1024) void k_scatter(Ws ws, int iter) {
     __hip_atomic_store(ws.hmir + 2, ws.ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 3, ws.ctl->remaining, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 4, ws.ctl->spec.on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 5, ws.ctl->spec_want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const Batch B = ws.ctl->cbat;
@@ -2079,6 +2080,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
         if (s_ser && s_specblk >= 0 && s_specool <= 0 && lowest_bucket(s_head, s_tail, 0) >= s_specblk) {
           if (lane == 0) s_specgo = 1;  // interrupt-dense: speculative generations from here on
         } else if (s_ser) {
+          if (ws.spec_lazy && lane == 0) ctl->spec_want = 1;  // the host allocates the engine
           serial_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, c4,
                       s_specblk > 0 ? s_specblk : 0, s_specblk >= 0 ? &s_specool : nullptr);
           wave_sync();

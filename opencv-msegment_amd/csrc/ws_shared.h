@@ -161,6 +161,9 @@ struct Ctl {
   unsigned rsv;      // epoch of the last batch k_resolve (or k_spec_flatten) decided
   int pad;
   SpecCtl spec;
+  int spec_want;     // the serial regime was entered while the speculative engine was enabled but
+                     // its workspace not yet allocated (Ws.spec_lazy): the host allocates it
+  int pad2;
 };
 
 static_assert(__builtin_offsetof(Ctl, error) % 8 == 0 && __builtin_offsetof(Ctl, rgive) == __builtin_offsetof(Ctl, error) + 4,
@@ -183,7 +186,7 @@ struct Ws {
   unsigned long long* cflag;  // per k_resolve chunk: {epoch, run} of its claim, epoch of its completion
   Ctl* ctl;
   unsigned long long* diag;  // nullptr = off; else 8 counters (msg_set_diag)
-  int* hmir;         // host-mapped progress mirror {iteration, done, error, remaining, spec} (k_scatter)
+  int* hmir;         // host-mapped progress mirror {iteration, done, error, remaining, spec, spec_want} (k_scatter)
   // speculative generations (nullptr when the engine is off); claims and labels are indexed by
   // tiled pixel like mk, one array of snp entries per round parity
   unsigned long long* scl;   // 2 x snp round claims {tag, rank, popped}
@@ -198,6 +201,7 @@ struct Ws {
   unsigned long long* sflag; // k_spec_flatten tile prefixes {generation tag, inclusive sum}
   long long snp;
   long long slogcap;
+  int spec_lazy;     // 1: engine enabled, workspace not allocated yet (k_scan reports spec_want)
   int H, W;
   int Wt;            // tiles per tile row = ceil(W / 4)
   int marg;          // tiled entries of margin before mk / w4 (mk - marg starts the state array)

@@ -43,6 +43,29 @@ public final class MSegmentNative {
     public static final int NC_BILATERAL = 0x8;
 
     /**
+     * The pre-filter and mask-size bits for notConnectedMarkers' options (PictureService.java:481-495),
+     * MEDIAN_BLUR winning over BILATERIAL as the reference's if / else-if.  MEDIAN_BLUR: medianBlur
+     * asserts ksize % 2 == 1 (negative and even sizes throw there), and sizes above 255 do not fit
+     * the option bits -- both throw instead of wrapping through the & 0xff packing.  BILATERIAL:
+     * sizes <= 0 act as 0 in bilateralFilter (sigma <= 0 -> 1), sizes above 255 throw.
+     */
+    public static int ncFilterBits(boolean medianBlur, boolean bilateral, int filterMaskSize) {
+        if (medianBlur) {
+            if (filterMaskSize < 1 || filterMaskSize % 2 != 1 || filterMaskSize > 255) {
+                throw new CvException("MEDIAN_BLUR mask size " + filterMaskSize + ": odd, 1..255");
+            }
+            return NC_MEDIAN_BLUR | (filterMaskSize << 8);
+        }
+        if (bilateral) {
+            if (filterMaskSize > 255) {
+                throw new CvException("BILATERIAL mask size " + filterMaskSize + ": at most 255");
+            }
+            return NC_BILATERAL | (Math.max(filterMaskSize, 0) << 8);
+        }
+        return 0;
+    }
+
+    /**
      * Drop-in for the marker stage of PictureService.notConnectedMarkers (PictureService.java:476-828):
      * returns wshedMarkSumm (CV_32SC1) and fills levelsOut with the BrightLevel list (the caller's
      * fThresholds; its size is the depth passed on to watershed / colorByIndexes).

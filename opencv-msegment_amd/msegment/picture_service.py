@@ -30,9 +30,14 @@ ColorResult = namedtuple("ColorResult", "dst bw labels depth sharp")
 def nc_option_flags(options, filter_mask_size):
     """msg_nc_marker_stage option bits for notConnectedMarkers' AlgorithmOptions
     (PictureService.java:469-495): GISTO_DIAP, MULTI_OTSU, and one pre-filter -- MEDIAN_BLUR wins
-    over BILATERIAL (the reference's if / else-if) -- with filterMaskSize in bits 8-15.  For
-    BILATERIAL every size <= 0 behaves as 0 in bilateralFilter (sigma <= 0 -> 1, radius
-    cvRound(1.5)), so it is passed as 0; sizes above 255 do not fit the option bits (MsegError)."""
+    over BILATERIAL (the reference's if / else-if) -- with filterMaskSize in bits 8-15.
+
+    MEDIAN_BLUR: OpenCV 3.4.2's medianBlur asserts ``ksize % 2 == 1`` (C++ remainder, so every
+    negative or even size throws CvException), so those raise MsegError here too; sizes above 255
+    are valid in OpenCV but do not fit the option bits (MsegError, never a silent wrap).
+    BILATERIAL: every size <= 0 behaves as 0 in bilateralFilter (sigma <= 0 -> 1, radius
+    cvRound(1.5)), so it is passed as 0; sizes above 255 do not fit the option bits (MsegError).
+    MSegmentNative.ncMaskBits is the same rule on the Java side."""
     from . import MsegError, _lib
 
     opts = set(options)
@@ -40,6 +45,11 @@ def nc_option_flags(options, filter_mask_size):
         _lib.MSG_NC_MULTI_OTSU if "MULTI_OTSU" in opts else 0)
     k = int(filter_mask_size)
     if "MEDIAN_BLUR" in opts:
+        if k < 1 or k % 2 != 1:
+            raise MsegError(_lib.MSG_EINVAL, "MEDIAN_BLUR mask size %d: must be odd and >= 1 "
+                            "(medianBlur's assertion)" % k)
+        if k > 255:
+            raise MsegError(_lib.MSG_EINVAL, "MEDIAN_BLUR mask size %d: at most 255" % k)
         flags |= _lib.MSG_NC_MEDIAN_BLUR | _lib.MSG_NC_MASK(k)
     elif "BILATERIAL" in opts:
         if k > 255:
@@ -164,8 +174,8 @@ class PictureService:
     def color_auto_marker_watershed(self, src, options=()):
         """PictureService.colorAutoMarkerWatershed (PictureService.java:301-392) on the GPU.
 
-        white -> black and src - 9x1 Laplacian (the sharpened image is what the watershed floods,
-        :333), Otsu bw, distanceTransform peaks, contours -> markers and depth = the contour
+        src - 9x1 Laplacian (the sharpened image is what the watershed floods, :333; the
+        white -> black loop :309-318 is a no-op in Java, PixelUtil.java:19's signed-byte compare), Otsu bw, distanceTransform peaks, contours -> markers and depth = the contour
         count (:355-364), then this.watershed(src, markers, depth, colored) (:378) and the
         bw_result (:384-386).  ``options``: COLORED changes the result; the save-step options do
         not apply here.  Returns ColorResult(dst, bw, labels = the flooded markers, depth, sharp).

@@ -5,7 +5,9 @@ flood's seeds for the colour method, restated step by step from OpenCV 3.4.2's d
 algorithms (OpenCV is an un-vendored Maven dependency, pom.xml:38-43: nothing here is pinned
 against a real OpenCV build -- "parity unpinned"):
 
-  :308-318  white (255,255,255) pixels -> black
+  :308-318  the "white -> black" loop is a NO-OP in Java: PixelUtil.checkPixelRGB
+            (PixelUtil.java:19) compares the signed byte of each channel (0xFF reads -1) with
+            int 255, which is never equal -- white pixels stay white
   :323-333  filter2D(src, CV_32F, MatOfFloat(1,1,1,1,-8,1,1,1,1)) -- a 9x1 COLUMN kernel,
             BORDER_REFLECT_101 -- then src - laplacian, saturated to CV_8UC3: exact integers,
             res = clamp(9 s(y) - sum_{0<|k|<=4} s(y+k), 0, 255) per channel; the result
@@ -42,10 +44,8 @@ def _reflect101(p, n):
 
 
 def sharpen(bgr):
-    """:308-333: white -> black, then src - filter2D(9x1 Laplacian), saturated."""
+    """:323-333: src - filter2D(9x1 Laplacian), saturated (white pixels kept: :309-318 is a no-op)."""
     s = np.asarray(bgr, dtype=np.int64).copy()
-    white = np.all(s == 255, axis=2)
-    s[white] = 0
     H = s.shape[0]
     acc = 9 * s
     for k in (-4, -3, -2, -1, 1, 2, 3, 4):

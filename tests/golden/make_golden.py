@@ -143,11 +143,17 @@ def write_digests(only=None):
 
 
 def write_album():
+    """The reference's resource images, decoded by PIL (RGB, palette expanded) and re-encoded
+    losslessly: the decoded pixels are the fixture (data), not the decoder."""
     from PIL import Image
 
-    src = "/root/reference/src/main/resources/images/album.jpg"
-    rgb = np.asarray(Image.open(src).convert("RGB"))
-    Image.fromarray(rgb).save(os.path.join(OUT, "album_1500x1500.png"), optimize=True)
+    res = "/root/reference/src/main/resources/images/"
+    for src, name in (("album.jpg", "album_1500x1500.png"), ("guide.png", None), ("haha.jpg", None)):
+        rgb = np.asarray(Image.open(res + src).convert("RGB"))
+        if name is None:
+            name = "%s_%dx%d.png" % (src.split(".")[0], rgb.shape[0], rgb.shape[1])
+        Image.fromarray(rgb).save(os.path.join(OUT, name), optimize=True)
+        print(name, rgb.shape, int(np.all(rgb == 255, axis=2).sum()), "white pixels")
 
 
 if __name__ == "__main__":

@@ -21,11 +21,26 @@ def test_sharpen_is_a_column_kernel_with_reflect101():
     assert C._reflect101(-1, 10) == 1 and C._reflect101(10, 10) == 8 and C._reflect101(-4, 2) == 0
 
 
-def test_white_becomes_black_before_the_filter():
+def _java_check_pixel_rgb(px, r, g, b):
+    """PixelUtil.checkPixelRGB (PixelUtil.java:19): Java's byte is signed, so a channel of 0xFF
+    reads -1 and is compared, widened to int, with the int literal 255."""
+    sb = np.asarray(px, np.uint8).astype(np.int8).astype(np.int64)
+    return bool(sb[0] == r and sb[1] == g and sb[2] == b)
+
+
+def test_white_to_black_loop_is_a_no_op_in_java():
+    # PictureService.java:309-318 calls checkPixelRGB(vec3b, 255, 255, 255): never true
+    assert not _java_check_pixel_rgb((255, 255, 255), 255, 255, 255)
+    assert _java_check_pixel_rgb((255, 255, 255), -1, -1, -1)  # what it would have needed
+    assert _java_check_pixel_rgb((0, 7, 127), 0, 7, 127)  # bytes below 0x80 compare as expected
+    # so an all-white frame keeps its white pixels: 9*255 - 8*255 = 255 in every channel
     img = np.full((5, 5, 3), 255, np.uint8)
-    assert not C.sharpen(img).any()
-    img[2, 2] = (255, 255, 254)  # not white: kept
-    assert C.sharpen(img)[2, 2, 2] > 0
+    assert (C.sharpen(img) == 255).all()
+    # and a white pixel in a dark column is sharpened as white (not as black)
+    img = np.zeros((9, 1, 3), np.uint8)
+    img[4, 0] = 255
+    out = C.sharpen(img)
+    assert (out[4, 0] == 255).all() and not out[[0, 1, 2, 3, 5, 6, 7, 8], 0].any()
 
 
 def test_otsu_first_maximum():

@@ -99,3 +99,29 @@ def test_color_auto_marker_watershed_pipeline(opts):
     assert np.array_equal(r.labels, labels)
     assert np.array_equal(r.dst, dst)
     assert np.array_equal(r.bw, ws_oracle.bgr2gray(dst))
+
+
+def _reference_image(name):
+    from PIL import Image
+
+    rgb = np.asarray(Image.open(os.path.join(os.path.dirname(__file__), "golden", name)).convert("RGB"))
+    return np.ascontiguousarray(rgb[:, :, ::-1])  # imread's BGR
+
+
+@pytest.mark.parametrize("name", ["album_1500x1500.png", "guide_225x225.png", "haha_373x400.png"])
+def test_color_pipeline_on_reference_images(name):
+    """App.java:28's colour method end to end on the reference's own pictures (every one holds
+    pure-white pixels, which the Java white -> black loop leaves white: PixelUtil.java:19)."""
+    img = _reference_image(name)
+    assert np.all(img == 255, axis=2).any()
+    ps = msegment.PictureService(seed=5)
+    r = ps.color_auto_marker_watershed(img, ())
+    sharp, mk, depth = C.color_markers(img)
+    assert np.array_equal(r.sharp, sharp), name
+    assert r.depth == depth, name
+    labels = ws_oracle.watershed(sharp, mk)
+    if not np.array_equal(r.labels, labels):
+        bad = np.argwhere(r.labels != labels)
+        raise AssertionError("%s: %d labels differ, first %s" % (name, len(bad), bad[0].tolist()))
+    dst = ws_oracle.colorize(labels, depth, None)
+    assert np.array_equal(r.dst, dst) and np.array_equal(r.bw, ws_oracle.bgr2gray(dst))

@@ -244,3 +244,13 @@ def test_nc_option_flags():
     assert np.array_equal(O.bilateral_tables(-4)[2], O.bilateral_tables(0)[2])
     with pytest.raises(msegment.MsegError):
         nc_option_flags(("BILATERIAL",), 256)
+    # MEDIAN_BLUR: medianBlur asserts ksize % 2 == 1 (C++ remainder: -1 % 2 == -1), so negative
+    # and even sizes throw in the reference; 257 is a valid median there but does not fit the
+    # option bits -- all rejected, none wrapped by the & 0xff packing (-1 -> 255, 257 -> 1)
+    assert nc_option_flags(("MEDIAN_BLUR",), 1) == _lib.MSG_NC_MEDIAN_BLUR | (1 << 8)
+    assert nc_option_flags(("MEDIAN_BLUR",), 255) == _lib.MSG_NC_MEDIAN_BLUR | (255 << 8)
+    for k in (-1, -255, 0, 4, 256, 257):
+        with pytest.raises(msegment.MsegError):
+            nc_option_flags(("MEDIAN_BLUR",), k)
+        with pytest.raises(msegment.MsegError):
+            nc_option_flags(("MEDIAN_BLUR", "BILATERIAL"), k)
