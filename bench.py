@@ -35,7 +35,10 @@ try:
     _hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
 except ValueError:
     _hwq = 0
-os.environ["GPU_MAX_HW_QUEUES"] = str(max(_hwq, 8))
+if os.environ.get("MSEG_BENCH_HWQ"):  # the batch_hwq4 child: exactly this many queues
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["MSEG_BENCH_HWQ"]
+else:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(max(_hwq, 8))
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "opencv-msegment_amd"))
@@ -54,6 +57,10 @@ BYTES_PER_PIXEL = {"k_prep": 15.0, "k_untile": 11.0, "k_colorize": 7.0, "k_edge_
 # k_resolve per item: queue entry 4 + own weights 4 + 4 neighbour states 16, out ipx 4 + granule 8
 # + desc 8 (push-competitor reads are data dependent and not counted)
 BYTES_PER_ITEM = {"k_resolve": 44.0}        # per batch item resolved
+# k_spec_round per execution (one item's top pop; cascade pops are data dependent, not counted):
+# queue entry 4 + own weights 4 + 4 neighbour states 16 in, claim 8 + label 4 + record 8 out
+BYTES_PER_EXEC = {"k_spec_round": 44.0}
+# k_serial per serial pop: queue entry 4 + own weights 4 + 4 neighbour states 16 in, label 4 out
 BYTES_SCATTER = (24.0, 8.0)                 # per committed item, per appended push
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")  # scripts/pmc_summary.py output
 E2E_BYTES_PER_PIXEL = 14.0                  # 3 B BGR + 4 B markers in, 4 B labels + 3 B BGR out
@@ -126,6 +133,8 @@ def kernel_roofline(prof, stats_per_step, npx, steps):
             alg = BYTES_PER_PIXEL[name] * npx * steps
         elif name in BYTES_PER_ITEM:
             alg = BYTES_PER_ITEM[name] * stats_per_step["items"] * steps
+        elif name in BYTES_PER_EXEC:
+            alg = BYTES_PER_EXEC[name] * stats_per_step["spec_executions"] * steps or None
         elif name == "k_scatter":
             alg = (BYTES_SCATTER[0] * stats_per_step["pops"] + BYTES_SCATTER[1] * stats_per_step["pushes"]) * steps
         else:
@@ -172,6 +181,9 @@ def cpu_baseline_nc(img, depth_opt, options, budget_s=12.0, max_reps=10):
         t_tot += time.perf_counter() - t0
         reps += 1
     return {"value": round(H * W * reps / t_tot / 1e6, 3), "unit": "Mpx/s", "cores": 1, "kind": "port",
+            "comparable": False,
+            "note": "numpy restatement of the marker stage, not an OpenCV-class C implementation: "
+                    "not comparable, no ratio quoted (the flood leg is the C oracle)",
             "sample": "%d full %dx%d frame(s): oracle/nc_oracle.py marker stage (numpy) + ws_oracle.c "
                       "watershed + colorize, 1 thread, %.1f s" % (reps, H, W, t_tot)}, lab
 
@@ -195,6 +207,9 @@ def cpu_baseline_shape(img, budget_s=12.0, max_reps=10, rows=512):
         t_tot += time.perf_counter() - t0
         reps += 1
     return {"value": round(H * W * reps / t_tot / 1e6, 3), "unit": "Mpx/s", "cores": 1, "kind": "port",
+            "comparable": False,
+            "note": "numpy/scipy restatement of the marker stage, not an OpenCV-class C implementation "
+                    "(OpenCV's O(1) median and SIMD Canny are far faster): not comparable, no ratio quoted",
             "sample": "%d band(s) of %dx%d (median %d as for the full frame): oracle/shape_oracle.py "
                       "marker stage (numpy/scipy) + ws_oracle.c watershed + colorize, 1 thread, %.1f s"
                       % (reps, H, W, k, t_tot)}, None
@@ -218,6 +233,9 @@ def cpu_baseline_color(img, budget_s=12.0, max_reps=10, rows=512):
         t_tot += time.perf_counter() - t0
         reps += 1
     return {"value": round(H * W * reps / t_tot / 1e6, 3), "unit": "Mpx/s", "cores": 1, "kind": "port",
+            "comparable": False,
+            "note": "numpy/scipy restatement of the marker stage, not an OpenCV-class C implementation: "
+                    "not comparable, no ratio quoted",
             "sample": "%d band(s) of %dx%d: oracle/color_oracle.py marker stage (numpy/scipy, C chamfer) + "
                       "ws_oracle.c watershed + colorize, 1 thread, %.1f s" % (reps, H, W, t_tot)}, None
 
@@ -253,6 +271,45 @@ def batch_throughput(seg, args, S, seed, sync, steps=5, warmup=2):
             "inflight": min(K, args.inflight), "steps": steps,
             "note": "BASELINE config 5 per GPU: %d frames (seeds %d..%d) per call, floods overlapped"
                     % (K, seed, seed + K - 1)}
+
+
+def batch_hwq4(args, S, seed):
+    """The batch line as a library user at the boxes' default of GPU_MAX_HW_QUEUES=4 gets it (this
+    process raised its own to 8 before HIP started): a child process with exactly 4 queues runs
+    the same batch at 2, 3 and 4 floods in flight."""
+    import subprocess
+
+    env = dict(os.environ, MSEG_BENCH_HWQ="4")
+    cmd = [sys.executable, os.path.abspath(__file__), "--batch-only", "--size", str(S), "--kind", args.kind,
+           "--seed", str(seed), "--batch-frames", str(args.batch_frames)]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+        line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+        return json.loads(line)
+    except Exception as e:  # noqa: BLE001 -- reported, not fatal to the headline line
+        return {"error": "batch_hwq4 child failed: %s" % e}
+
+
+def batch_only(args):
+    """--batch-only (the batch_hwq4 child): batch throughput at 2, 3, 4 floods in flight."""
+    import torch
+
+    import msegment
+
+    torch.cuda.set_device(0)
+    seg = msegment.Segmenter(0)
+    sync = torch.cuda.synchronize
+    rows = {}
+    for k in (2, 3, 4):
+        args.inflight = k
+        rows[str(k)] = batch_throughput(seg, args, args.size, args.seed, sync)["value"]
+    seg.close()
+    best = max(rows, key=lambda k: rows[k])
+    print(json.dumps({"value": rows[best], "unit": "Mpx/s", "inflight": int(best), "by_inflight": rows,
+                      "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                      "note": "the batch line at the boxes' default GPU_MAX_HW_QUEUES=4 (child process)"}),
+          flush=True)
+    return 0
 
 
 def batch_cpu_threads(K):
@@ -315,13 +372,39 @@ def stress_line(seg, S, sync, dev, steps, cpu=True, kind="mosaic_noise", seed=2)
         seg.watershed_colorize_dev(t_img, t_m, t_lab, depth, None, t_dst)
     sync()
     dt = time.perf_counter() - t0
+    value = S * S * steps / dt / 1e6
     out = {"workload": "%s %dx%d seed %d, watershed + colorByIndexes(colored=false), device-resident "
                        "(BASELINE config 3 stress variant)" % (kind, S, S, seed),
-           "value": round(S * S * steps / dt / 1e6, 3), "unit": "Mpx/s", "steps": steps,
-           "ms_per_step": round(1000.0 * dt / steps, 3), "parity": parity,
-           "flood": {"batches": st["batches"], "pops": st["pops"], "items": st["items"],
-                     "spec_generations": st["spec_generations"], "spec_rounds": st["spec_rounds"],
-                     "spec_executions": st["spec_executions"], "spec_fallbacks": st["spec_fallbacks"]}}
+           "value": round(value, 3), "unit": "Mpx/s", "steps": steps,
+           "ms_per_step": round(1000.0 * dt / steps, 3), "parity": parity}
+    # the dominant kernel of the same step, HIP-event timed (one profiled step); the flood's
+    # counters from that step (the first flood of a context may run part of the way without the
+    # speculative engine, which is allocated on first use)
+    seg.set_profiling(True)
+    seg.kernel_profile(reset=True)
+    seg.watershed_colorize_dev(t_img, t_m, t_lab, depth, None, t_dst)
+    sync()
+    prof = seg.kernel_profile(reset=True)
+    seg.set_profiling(False)
+    st = seg.stats()
+    out["flood"] = {"batches": st["batches"], "pops": st["pops"], "items": st["items"],
+                    "spec_generations": st["spec_generations"], "spec_rounds": st["spec_rounds"],
+                    "spec_executions": st["spec_executions"], "spec_fallbacks": st["spec_fallbacks"],
+                    "executions_per_pop": round(st["spec_executions"] / max(1, st["pops"]), 3)}
+    kern = kernel_roofline(prof, st, S * S, 1)
+    out["kernels"] = kern
+    top = kern[0] if kern else None
+    e2e = value * 1e6 * E2E_BYTES_PER_PIXEL / 1e9
+    roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "e2e_achieved": round(e2e, 3), "e2e_frac": round(e2e / HBM_PEAK_GBS, 6)}
+    if top:
+        traffic, tsrc = pmc_traffic(top["kernel"], {"pipeline": "watershed", "kind": kind, "size": S, "seed": seed,
+                                                    "frames": 1})
+        roof.update({"kernel": top["kernel"], "achieved": top["achieved_gbs"],
+                     "frac": round(top["achieved_gbs"] / HBM_PEAK_GBS, 6) if top["achieved_gbs"] else None,
+                     "alg_bytes_per_launch": top["alg_bytes_per_launch"], "avg_launch_us": top["avg_us"],
+                     "launches": round(top["launches_per_step"], 1), "traffic": traffic, "traffic_source": tsrc})
+    out["roofline"] = roof
     if cpu:
         c, cl = cpu_baseline(img, m, depth, budget_s=8.0, max_reps=5)
         out["cpu_baseline"] = c
@@ -332,15 +415,19 @@ def stress_line(seg, S, sync, dev, steps, cpu=True, kind="mosaic_noise", seed=2)
 
 
 def pmc_traffic(kernel, cfg):
-    """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/pmc_latest.json,
-    scripts/pmc_summary.py), only when they were collected on this same workload `cfg`."""
-    if not os.path.exists(PMC_SUMMARY):
-        return None, None
-    pm = json.load(open(PMC_SUMMARY))
-    kk = pm.get("kernels", {}).get(kernel)
-    if not kk or pm.get("config") != cfg:
-        return None, None
-    return round(kk["hbm_bytes_per_launch"]), "profiles/pmc_latest.json (%s; %s)" % (pm.get("correction"), pm.get("note", ""))
+    """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/pmc_*.json,
+    scripts/pmc_summary.py), only from a file collected on this same workload `cfg`."""
+    import glob
+
+    for path in [PMC_SUMMARY] + sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+        if not os.path.exists(path):
+            continue
+        pm = json.load(open(path))
+        kk = pm.get("kernels", {}).get(kernel)
+        if kk and pm.get("config") == cfg:
+            return round(kk["hbm_bytes_per_launch"]), "%s (%s; %s)" % (
+                os.path.relpath(path, ROOT), pm.get("correction"), pm.get("note", ""))
+    return None, None
 
 
 def colour_distance(seg, t_img, img, S, sync, pmc_cfg, reps=20, check=True):
@@ -448,7 +535,13 @@ def main(argv=None):
                     help="steps of the config-3 stress line (mosaic+noise at --size); 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile-pass", action="store_true")
+    ap.add_argument("--batch-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-hwq4", action="store_true", help="skip the batch_hwq4 child process")
     args = ap.parse_args(argv)
+    if args.batch_only:
+        if args.seed is None:
+            args.seed = 100
+        return batch_only(args)
     # the nc pipeline's scattered seeds put the flood in its slowest regime
     if args.steps is None:
         args.steps = 2 if args.pipeline in ("nc", "color") else 10
@@ -588,10 +681,15 @@ def main(argv=None):
         batch = batch_throughput(seg, args, S, bseed, sync)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             batch["cpu_baseline"] = cpu_baseline_batch(args.kind, S, bseed, args.batch_frames)
+        if rank == 0 and world == 1 and not args.no_hwq4:
+            batch["hwq4"] = batch_hwq4(args, S, bseed)
 
-    stress = None
+    stress = stress_random = None
     if rank == 0 and world == 1 and K == 1 and not MARKERS and args.kind == "mosaic" and args.stress_steps > 0:
         stress = stress_line(seg, S, sync, dev, args.stress_steps, cpu=not args.no_cpu_baseline)
+        # the uniform-random variant (config 3's worst case), fewer steps
+        stress_random = stress_line(seg, S, sync, dev, max(1, args.stress_steps // 2),
+                                    cpu=not args.no_cpu_baseline, kind="random")
 
     pcie = None
     if rank == 0 and world == 1 and not MARKERS:
@@ -657,6 +755,7 @@ def main(argv=None):
             "colour_distance": stencil,
             "batch": batch,
             "stress": stress,
+            "stress_random": stress_random,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
             "e2e_hbm": {"achieved": round(e2e_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

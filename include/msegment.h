@@ -74,7 +74,7 @@ typedef struct msg_stats {
     int64_t spec_fallbacks;     /* overflowing executions handed to serial pops                 */
 } msg_stats;
 
-#define MSG_NKERNELS 22
+#define MSG_NKERNELS 24
 typedef struct msg_kernel_profile {
     char    name[32];       /* kernel name, e.g. "k_resolve"                                   */
     int64_t launches;       /* launches timed since the last reset                              */
@@ -97,12 +97,24 @@ int  msg_get_kernel_profile(msg_ctx* ctx, msg_kernel_profile* out, int max_entri
 /* In-kernel cycle counters (s_memtime) for the flood kernels, reported in msg_stats.diag.
  * Diagnostics only: they add atomics to the kernels; never enabled in timed runs.
  * enable == 2 also injects faults for tests: the decision kernel's odd blocks give up their
- * first chunk of every batch once, which exercises the give-up / re-run path. */
+ * first chunk of every batch once, which exercises the give-up / re-run path.
+ * enable == 3 reports the regime split instead: tiny batches, their pops, their time
+ * (s_memrealtime, 10 ns ticks); serial pops, their time; k_serial launches that popped, their
+ * LDS line fills; pops of small batches (65..4096 items). */
 int  msg_set_diag(msg_ctx* ctx, int enable);
 /* Speculative generations for the interrupt-dense regime (textured frames, scattered seeds):
  * on by default.  enable = 0 keeps the batch engine's serial pops there instead (A/B runs and
  * tests of that path).  Results are identical either way (both are the exact serial order). */
 int  msg_set_speculative(msg_ctx* ctx, int enable);
+/* Two-launch flood iterations for large batches (decide, then one commit grid that also forms
+ * the next batch) instead of three (decide, one-block scan, scatter): on by default; 0 keeps
+ * the three-launch iterations (A/B runs and tests).  Results are identical either way. */
+int  msg_set_fast_commit(msg_ctx* ctx, int enable);
+/* The serial-pop regime (interrupt-dense floods: real photographs, scattered seeds) in a kernel of
+ * its own with the flood state cached in LDS (k_serial) instead of inside the one-workgroup batch
+ * loop.  Off by default: measured no faster per pop yet.  Results are
+ * identical either way. */
+int  msg_set_serial_kernel(msg_ctx* ctx, int enable);
 
 /* ---- host-buffer entry points (synchronous; strides in BYTES) ---------------------------- */
 

@@ -48,6 +48,8 @@ struct msg_ctx {
   unsigned long long *d_tl = nullptr, *d_desc = nullptr, *d_cflag = nullptr;
   long long qcap = 0;
   // speculative generations (spec_kernels.hip): allocated on the first flood that may use them
+  bool fast = true;             // msg_set_fast_commit: two-launch iterations for large batches
+  bool serk = false;            // msg_set_serial_kernel: serial pops in k_serial (LDS-cached state)
   bool spec = true;             // msg_set_speculative
   long long spec_np = 0, spec_logcap = 0;
   unsigned long long *d_scl = nullptr, *d_sfin = nullptr, *d_stl = nullptr, *d_slog = nullptr;
@@ -78,6 +80,7 @@ struct msg_ctx {
   bool prof = false;
   unsigned long long* d_diag = nullptr;  // 8 counters when diagnostics are on
   bool diag = false;
+  int diag_bank = 0;  // msg_set_diag(ctx, 3): report the small-batch loop's regime split (bank 2)
   int inject = 0;  // msg_set_diag(ctx, 2): k_resolve give-up injection (tests)
   std::vector<hipEvent_t> evpool;
   size_t evused = 0;
@@ -123,14 +126,15 @@ namespace {
 enum KernelId { KID_PREP, KID_INIT_SCAN, KID_COMPACT, KID_RESOLVE, KID_SCAN, KID_SCATTER,
                 KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_GRAY_HIST, KID_NC_MARKERS, KID_SPEC_ROUND,
                 KID_GRAY, KID_MEDIAN, KID_CANNY, KID_CCL, KID_RING, KID_NUMBER, KID_HOLES, KID_SPEC_FLATTEN,
-                KID_COLOR, KID_BILATERAL };
+                KID_COLOR, KID_BILATERAL, KID_COMMIT_FAST, KID_SERIAL };
 const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_compact", "k_resolve",
                                                 "k_scan", "k_scatter", "k_colorize",
                                                 "k_edge_weights", "k_untile", "k_gray_hist",
                                                 "k_nc_markers", "k_spec_round", "k_gray",
                                                 "k_median", "k_canny_nms", "k_ccl", "k_ring_median3",
                                                 "k_cc_number", "k_holes", "k_spec_flatten",
-                                                "k_color_stage", "k_bilateral"};
+                                                "k_color_stage", "k_bilateral", "k_commit_fast",
+                                                "k_serial"};
 
 hipEvent_t pool_event(msg_ctx* c) {
   if (c->evused == c->evpool.size()) {
@@ -398,6 +402,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   ws.diag = c->diag ? c->d_diag : nullptr;
 
   ws.hmir = c->d_mir;
+  ws.serk = c->serk ? 1 : 0;
   ws.H = H;
   ws.W = W;
   ws.Wt = (W + 3) / 4;
@@ -433,7 +438,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   const int gsc = std::min(npx * (CH / 1024), 1024);
   HIPCHK(c, hipMemsetAsync(c->d_ctl, 0, sizeof(Ctl), st));
   HIPCHK(c, hipMemsetAsync(c->d_capp, 0, (size_t)CAP_SLOTS * NQ * 4, st));
-  if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 16 * sizeof(unsigned long long), st));
+  if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 24 * sizeof(unsigned long long), st));
   HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)npx * NQ * sizeof(int32_t), st));
   const int nrc = H * ws.nseg;  // raster chunks
   // k_prep4 (one thread per tile) where widths and buffers allow 12-B / 16-B quad loads
@@ -453,7 +458,10 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   __atomic_store_n(&c->h_mir[0], -1, __ATOMIC_RELEASE);
   c->h_mir[4] = 0;
   c->h_mir[5] = 0;
+  c->h_mir[6] = 0;
+  c->h_mir[7] = 0;
   int it = 0, prev_end = -1;
+  bool ser_seen = false;
   c->group = 4;
   long long syncs = 0;
   // Two kinds of iteration, chosen per group from the regime the last poll reported (a stale
@@ -464,7 +472,26 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   const int gflat = std::max(1, c->cus);
   for (;;) {
     const bool spec_it = spec_bound && c->h_mir[4] != 0;
+    // two-launch iterations while the last report was a large flood batch (k_commit_fast)
+    const bool fast_it = !spec_it && c->fast && c->h_mir[6] != 0;
+    const bool ser_it = !spec_it && c->serk && c->h_mir[7] != 0;
+    // once this flood has entered the serial regime, every three-launch iteration ends with a
+    // k_serial (a no-op unless that iteration's k_scan handed the regime over), so the hand-over
+    // does not wait for the host to see it
+    ser_seen = ser_seen || (c->serk && c->h_mir[7] != 0);
     for (int g = 0; g < c->group; ++g, ++it) {
+      if (ser_it) {  // serial pops pending: one wave with the LDS-cached state
+        LAUNCH(c, KID_SERIAL, st, k_serial, dim3(1), dim3(64), 0, ws, it);
+        continue;
+      }
+      if (fast_it) {
+        if (c->inject)  // test only: give-ups (msg_set_diag 2) -> k_commit_fast schedules re-runs
+          LAUNCH(c, KID_RESOLVE, st, k_resolve<true>, dim3(gres), dim3(RBS), 0, ws);
+        else
+          LAUNCH(c, KID_RESOLVE, st, k_resolve<false>, dim3(gres), dim3(RBS), 0, ws);
+        LAUNCH(c, KID_COMMIT_FAST, st, k_commit_fast, dim3(FAST_SUBS + 1), dim3(1024), 0, ws, it);
+        continue;
+      }
       if (spec_it) {
         for (int r = 0; r < SPEC_ITER_ROUNDS; ++r)
           LAUNCH(c, KID_SPEC_ROUND, st, k_spec_round, dim3(c->spec_grid), dim3(SPEC_BS), 0, ws);
@@ -476,6 +503,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
       }
       LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);  // + small batches
       LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, it);
+      if (ser_seen) LAUNCH(c, KID_SERIAL, st, k_serial, dim3(1), dim3(64), 0, ws, it);
     }
     HIPCHK(c, hipGetLastError());
     if (prev_end >= 0) {
@@ -509,7 +537,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   }
   Ctl tail;
   HIPCHK(c, hipMemcpyAsync(&tail, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
-  unsigned long long dgv[16] = {0};
+  unsigned long long dgv[24] = {0};
   if (c->diag) HIPCHK(c, hipMemcpyAsync(dgv, c->d_diag, sizeof(dgv), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
   ++syncs;
@@ -519,7 +547,8 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   c->stats.items = tail.items;
   c->stats.pushes = tail.pushes;
   // when speculative generations ran, diag reports their round split instead (spec_kernels.hip)
-  for (int k = 0; k < 8; ++k) c->stats.diag[k] = (int64_t)dgv[tail.spec.gens ? 8 + k : k];
+  for (int k = 0; k < 8; ++k)
+    c->stats.diag[k] = (int64_t)dgv[c->diag_bank == 2 ? 16 + k : tail.spec.gens ? 8 + k : k];
   c->stats.host_syncs = syncs;
   c->stats.spec_generations = tail.spec.gens;
   c->stats.spec_rounds = tail.spec.rounds_total;
@@ -617,6 +646,8 @@ int run_batch(msg_ctx* c, int n, F fn) {
   for (int w = 0; w < k; ++w) {
     c->subs[w]->res_grid = c->res_grid;
     c->subs[w]->spec = c->spec;
+    c->subs[w]->fast = c->fast;
+    c->subs[w]->serk = c->serk;
     if (c->subs[w]->diag != c->diag || c->subs[w]->inject != c->inject) {
       rc = msg_set_diag(c->subs[w], c->inject ? 2 : c->diag ? 1 : 0);
       if (rc) return rc;
@@ -886,6 +917,20 @@ int msg_get_stats(const msg_ctx* c, msg_stats* out) {
   return MSG_OK;
 }
 
+int msg_set_fast_commit(msg_ctx* c, int enable) {
+  if (!c) return MSG_EINVAL;
+  c->fast = enable != 0;
+  for (msg_ctx* sub : c->subs) sub->fast = c->fast;
+  return MSG_OK;
+}
+
+int msg_set_serial_kernel(msg_ctx* c, int enable) {
+  if (!c) return MSG_EINVAL;
+  c->serk = enable != 0;
+  for (msg_ctx* sub : c->subs) sub->serk = c->serk;
+  return MSG_OK;
+}
+
 int msg_set_speculative(msg_ctx* c, int enable) {
   if (!c) return MSG_EINVAL;
   c->spec = enable != 0;
@@ -907,10 +952,11 @@ int msg_set_diag(msg_ctx* c, int enable) {
   if (!c) return MSG_EINVAL;
   if (enable && !c->d_diag) {
     HIPCHK(c, hipSetDevice(c->dev));
-    HIPCHK(c, hipMalloc((void**)&c->d_diag, 16 * sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc((void**)&c->d_diag, 24 * sizeof(unsigned long long)));
   }
   c->diag = enable != 0;
   c->inject = enable == 2;
+  c->diag_bank = enable == 3 ? 2 : 0;
   return MSG_OK;
 }
 

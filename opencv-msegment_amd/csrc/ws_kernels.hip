@@ -720,6 +720,12 @@ __device__ void form_batch(const int* qbase, const int* head, const int* tail, i
   }
 }
 
+// A batch the two-launch iterations (k_resolve -> k_commit_fast) suit: a flood batch too large
+// for k_scan's one-workgroup loop, and within k_commit_fast's chunk limit.
+__device__ __forceinline__ bool fast_batch(const Batch& b) {
+  return b.mode == 0 && b.n > SMALL_MAX && b.n <= FAST_CH * CH;
+}
+
 // rank -> segment (segments sorted by rank); slot -> batch rank or -1 (sorted by bstart too:
 // bucket regions are laid out in level order).
 __device__ __forceinline__ int seg_of_rank(const Seg* s, int nseg, int r) {
@@ -1144,12 +1150,17 @@ __device__ __attribute__((noinline)) bool orphan_below(const unsigned long long*
 template <bool INJECT>
 __global__ __launch_bounds__(RBS, 4) void k_resolve(Ws ws) {
   Ctl* ctl = ws.ctl;
-  const Batch B = ctl->bat;
-  const bool work = !(B.n == 0 || B.mode != 0 || ctl->error);
   __shared__ Seg segs[NQ];
   __shared__ int hist[NQ];
   __shared__ int s_minpush;
-  if (work) load_segs(ctl, B, segs);
+  // the first segments are loaded together with the batch header (most batches have one), the
+  // rest -- of a multi-segment batch -- once its size is known
+  if (threadIdx.x < 4) segs[threadIdx.x] = ctl->seg[threadIdx.x];
+  const Batch B = ctl->bat;
+  // hold: k_commit_fast declined this decided batch (too many chunks); k_scan commits it
+  const bool work = !(B.n == 0 || B.mode != 0 || ctl->error || ctl->hold == B.epoch);
+  if (work)
+    for (int k = 4 + threadIdx.x; k < B.nseg; k += blockDim.x) segs[k] = ctl->seg[k];
   if (threadIdx.x == 0) s_minpush = NQ;
   const int tid = threadIdx.x, lane = lane_id();
   const unsigned long long etag = (unsigned long long)B.epoch << 32;  // final label granule
@@ -1435,7 +1446,7 @@ __device__ Batch scan_body(const Ws& ws) {
     }
     return none;
   }
-  if (B.mode == 3 || (B.mode == 0 && ctl->rsv != B.epoch)) {
+  if (B.mode == 3 || B.mode == 4 || (B.mode == 0 && ctl->rsv != B.epoch)) {
     // not decided yet: speculative rounds still running, or an iteration without k_resolve
     // (the host queued the other iteration kind): nothing to commit here
     __syncthreads();
@@ -1680,11 +1691,279 @@ __global__ __launch_bounds__(1024) void k_scatter(Ws ws, int iter) {
     __hip_atomic_store(ws.hmir + 3, ws.ctl->remaining, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 4, ws.ctl->spec.on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 5, ws.ctl->spec_want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 6, fast_batch(ws.ctl->bat) ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 7, ws.ctl->bat.mode == 4 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const Batch B = ws.ctl->cbat;
   if (B.nchunk == 0 || ws.ctl->error) return;
   scatter_chunks(ws, B, blockIdx.x, gridDim.x);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Two-launch iterations for large batches (k_resolve -> k_commit_fast): the commit of k_scan and
+// k_scatter in one grid.  Blocks 0 .. FAST_CH*SUBS-1 each take one 1024-item sub-round and compute
+// its bucket offsets themselves -- the old tails plus the histogram rows of the earlier chunks (at
+// most FAST_CH rows, L2-resident) plus the chunk's earlier sub-rounds, recounted from their
+// descriptors -- so no column scan has to finish first.  The last block is the FINALIZER: it forms
+// the next batch from the same control words and rows (all its reads overlap the scatter), then
+// waits until every sub-round block has ARRIVED -- reported after that block's last read of the
+// control block and of the rows, on one of 8 counters by blockIdx % 8 (a single counter costs
+// ~12 ns per arrival) -- and only then rewrites the queue state and zeroes the rows.  The grid
+// (FAST_SUBS + 1 = 481 blocks of 1024 threads, two per CU) is resident at once.  No fence is
+// needed: the finalizer reads only what k_resolve wrote, and the arrivals only order reads before
+// writes.  Batches it cannot commit are left alone: not decided yet (a speculative generation, or
+// the host queued this iteration kind on stale information) -- nothing happens; decided but over
+// FAST_CH chunks -- `hold` stops k_resolve from deciding it again and k_scan commits it.  k_scan's
+// one-workgroup loop for runs of small batches is not here: the host goes back to three-launch
+// iterations when the progress mirror reports a batch that is not fast_batch.
+constexpr int FAST_SUBS = FAST_CH * (CH / 1024);  // sub-round blocks; the grid is FAST_SUBS + 1
+
+// sum of cnt[c][lv] over the rows c < nrows with c % 4 == g (nrows <= FAST_CH): all loads first
+__device__ __forceinline__ int rows_sum(const int* cnt, int g, int nrows, int lv) {
+  int v[FAST_CH / 4];
+#pragma unroll
+  for (int k = 0; k < FAST_CH / 4; ++k) {
+    const int c = g + 4 * k;
+    v[k] = (c < nrows) ? cnt[(long long)c * NQ + lv] : 0;
+  }
+  int sum = 0;
+#pragma unroll
+  for (int k = 0; k < FAST_CH / 4; ++k) sum += v[k];
+  return sum;
+}
+
+// What the commit of the current batch is: 1 commit ncommit items, 2 re-run (a k_resolve block
+// gave its chunk up), 4 decided but too large (k_scan commits it), 0 nothing to do.
+__device__ __forceinline__ int fast_flags(const Ctl* ctl, const Batch& B, int& ncommit) {
+  const unsigned rsv = ctl->rsv, hold = ctl->hold;
+  const int err = ctl->error, give = ctl->rgive, cut = ctl->cut, segcut = ctl->segcut;
+  ncommit = 0;
+  const bool decided = B.mode == 0 && B.n > 0 && rsv == B.epoch && !err && hold != B.epoch;
+  if (!decided) return 0;
+  if (give) return 2;
+  if (B.n > FAST_CH * CH) return 4;
+  ncommit = B.n;
+  if (cut != NONE) ncommit = min(ncommit, cut + 1);
+  if (segcut != NONE) ncommit = min(ncommit, ctl->seg[segcut].rank);
+  return 1;
+}
+
+__global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
+  Ctl* ctl = ws.ctl;
+  constexpr int NW = 16, SUBS = CH / 1024;
+  __shared__ int run[NQ], qb[NQ], gpart[4][NQ];
+  __shared__ int wcnt[NW][NQ];
+  __shared__ Batch s_B;
+  __shared__ int s_ncommit, s_flags;
+  const int tid = threadIdx.x, wv = tid >> 6;
+  const int Wt = ws.Wt;
+  if (tid == 0) {
+    const Batch B = ctl->bat;
+    int ncommit;
+    s_flags = fast_flags(ctl, B, ncommit);
+    s_ncommit = ncommit;
+    s_B = B;
+  }
+  if (tid < NQ) qb[tid] = ctl->qbase[tid];
+  __syncthreads();
+  const Batch B = s_B;
+  const int ncommit = s_ncommit, flags = s_flags;
+  unsigned* const arrive = (unsigned*)&ctl->farrive[0];
+  if (blockIdx.x < FAST_SUBS) {
+    // ---- a sub-round block ----
+    const int vb = blockIdx.x, ch = vb / SUBS, i0 = ch * CH + (vb % SUBS) * 1024;
+    if (!(flags & 1) || i0 >= ncommit) {  // block-uniform: nothing to scatter, done reading
+      if (tid == 0) atomicAdd(&arrive[blockIdx.x & 7], 1u);
+      return;
+    }
+    // rows of the earlier chunks: a quarter per thread group, every load issued before the sums
+    gpart[tid >> 8][tid & (NQ - 1)] = rows_sum(ws.cnt, tid >> 8, ch, tid & (NQ - 1));
+    if (tid < NQ) {
+#pragma unroll
+      for (int k = 0; k < NW; ++k) wcnt[k][tid] = 0;
+    }
+    __syncthreads();
+    if (tid < NQ) run[tid] = ctl->qtail[tid] + gpart[0][tid] + gpart[1][tid] + gpart[2][tid] + gpart[3][tid];
+    __syncthreads();  // this block's reads of the control block and of the rows are complete
+    if (tid == 0) atomicAdd(&arrive[blockIdx.x & 7], 1u);
+    for (int j = ch * CH + tid; j < i0; j += 1024) {  // earlier sub-rounds of this chunk
+      const unsigned long long d = ws.desc[j];
+      const unsigned m = (unsigned)(d >> 32) & 15u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if ((m >> k) & 1u) atomicAdd(&run[(d >> (8 * k)) & 255], 1);
+    }
+    const int i = i0 + tid;
+    const bool valid = i < ncommit;
+    unsigned mask = 0, lvls = 0;
+    long long p = 0;
+    if (valid) {
+      const unsigned long long d = ws.desc[i];
+      mask = (unsigned)(d >> 32) & 15u;
+      lvls = (unsigned)d;
+      p = ws.ipx[i];
+      st_state(ws, p, (int32_t)(uint32_t)ws.tl[i]);
+    }
+    int pos[4] = {0, 0, 0, 0};
+    wave_rank(mask, lvls, pos, wcnt[wv]);
+    __syncthreads();
+    if (tid < NQ) {
+      int acc = run[tid];
+#pragma unroll
+      for (int k = 0; k < NW; ++k) {
+        const int t = wcnt[k][tid];
+        wcnt[k][tid] = acc;
+        acc += t;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      if (!((mask >> d) & 1u)) continue;
+      const int lv = (lvls >> (8 * d)) & 255;
+      const int dest = qb[lv] + wcnt[wv][lv] + pos[d];
+      if (dest < 0 || (long long)dest >= ws.qcap) {
+        atomicOr(&ctl->error, ERR_CAPACITY);
+        continue;
+      }
+      const long long n = nb_of(p, d, Wt);
+      st_state(ws, n, queued_state(dest));
+      ws.qbuf[dest] = (int32_t)n;
+    }
+    return;
+  }
+  // ---- the finalizer ----
+  __shared__ int s_head[NQ], s_tail[NQ], partial[NQ];
+  __shared__ Seg nsegs[NQ];
+  __shared__ int s_nseg, s_n, s_wcap, s_minpush;
+  if (flags & 1) {
+    const int nch = (ncommit + CH - 1) / CH;
+    const bool haspartial = (ncommit % CH) != 0 && ncommit != B.n;
+    if (tid < NQ) {
+      s_head[tid] = ctl->qhead[tid];
+      s_tail[tid] = ctl->qtail[tid];
+      partial[tid] = 0;
+    }
+    if (tid == 0) {
+      s_wcap = next_wcap(ctl->wcap, B.n, ncommit, ctl->cut != NONE && ncommit == ctl->cut + 1);
+      s_minpush = ctl->minpush;
+    }
+    __syncthreads();
+    if (haspartial) {  // the cut chunk's row counts items past the cut: recount its prefix
+      for (int i = (nch - 1) * CH + tid; i < ncommit; i += 1024) {
+        const unsigned long long d = ws.desc[i];
+        const unsigned m = (unsigned)(d >> 32) & 15u;
+        for (int k = 0; k < 4; ++k)
+          if ((m >> k) & 1u) atomicAdd(&partial[(d >> (8 * k)) & 255], 1);
+      }
+    }
+    gpart[tid >> 8][tid & (NQ - 1)] = rows_sum(ws.cnt, tid >> 8, haspartial ? nch - 1 : nch, tid & (NQ - 1));
+    __syncthreads();
+    int dp = 0;
+    if (tid < NQ) {
+      dp = gpart[0][tid] + gpart[1][tid] + gpart[2][tid] + gpart[3][tid] + partial[tid];
+      s_tail[tid] += dp;
+    }
+    if (tid < B.nseg) {  // advance every segment's bucket head by what it committed
+      const Seg sg = ctl->seg[tid];
+      atomicAdd(&s_head[sg.L], max(0, min(ncommit - sg.rank, sg.n)));
+    }
+    if (tid < NQ) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) dp += __shfl_xor(dp, o);
+      if ((tid & 63) == 0 && dp) atomicAdd((unsigned long long*)&ctl->pushes, (unsigned long long)dp);
+    }
+    __syncthreads();
+    form_batch(qb, s_head, s_tail, s_minpush, s_wcap, nsegs, &s_nseg, &s_n);
+  }
+  // wait for every sub-round block's arrival -- each arrives once it has read the control block,
+  // whether or not it has a sub-round to scatter (a block starting after the finalizer wrote would
+  // read the next batch's words).  The grid fits the device at once (FAST_SUBS + 1 blocks of 1024
+  // threads, two per CU), and sub-round blocks never wait, so they all get to run.
+  if (tid < 64) {
+    const int expect = FAST_SUBS;
+    long long t0 = 0;
+    for (;;) {
+      unsigned v = (tid < 8) ? __hip_atomic_load(&arrive[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+      for (int o = 4; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      v = __shfl(v, 0);
+      if ((int)v >= expect) break;
+      __builtin_amdgcn_s_sleep(1);
+      const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+      if (t0 == 0) t0 = now;
+      else if (now - t0 > SPIN_LIMIT_TICKS) {
+        if (tid == 0) atomicOr(&ctl->error, ERR_TIMEOUT);
+        break;
+      }
+    }
+    if (tid < 8) arrive[tid] = 0u;  // every arrival is in: reset for the next launch
+  }
+  __syncthreads();
+  if (flags & 1) {
+    // the rows k_resolve accumulated are consumed: zero them for the next batch
+    const long long rows = (long long)((B.n + CH - 1) / CH) * NQ;
+    for (long long k = tid; k < rows; k += 1024) ws.cnt[k] = 0;
+    const int ns = s_nseg;
+    for (int k = tid; k < ns; k += 1024) ctl->seg[k] = nsegs[k];
+    if (tid < NQ) {
+      ctl->qhead[tid] = s_head[tid];
+      ctl->qtail[tid] = s_tail[tid];
+    }
+    if (tid < 64) {  // queued items left (host polling hint)
+      int q = 0;
+#pragma unroll
+      for (int k = 0; k < NQ / 64; ++k) q += s_tail[tid + 64 * k] - s_head[tid + 64 * k];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+      if (tid == 0) ctl->remaining = q;
+    }
+    if (tid == 0) {
+      ctl->pops += ncommit;
+      ctl->items += B.n;
+      Batch nb;
+      nb.mode = 0;
+      nb.epoch = B.epoch + 1;
+      nb.ncommit = 0;
+      nb.nchunk = 0;
+      nb.rrun = 0;
+      nb.nseg = ns;
+      nb.n = (ns > 0) ? s_n : 0;
+      nb.L = (ns > 0) ? nsegs[0].L : -1;
+      nb.bstart = (ns > 0) ? nsegs[0].bstart : 0;
+      if (ns > 0 && ctl->spec.on)
+        spec_begin(ctl, nb, nsegs[0].L, nsegs[0].bstart, s_tail[nsegs[0].L] - s_head[nsegs[0].L]);
+      ctl->bat = nb;
+      ctl->cbat.n = 0;
+      ctl->cbat.nchunk = 0;
+      ctl->wcap = s_wcap;
+      ctl->cut = NONE;
+      ctl->segcut = NONE;
+      ctl->minpush = NQ;
+      if (ns > 0) ctl->batches += 1;
+      else ctl->done = 1;
+    }
+  } else if (tid == 0) {
+    if (flags & 2) {
+      ctl->rgive = 0;
+      ctl->bat.rrun = B.rrun + 1;
+    } else if (flags & 4) {
+      ctl->hold = B.epoch;
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && ws.hmir) {
+    const Batch nb = ctl->bat;
+    __hip_atomic_store(ws.hmir + 1, ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 2, ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 3, ctl->remaining, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 4, ctl->spec.on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 5, ctl->spec_want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 6, fast_batch(nb) ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 7, nb.mode == 4 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1954,6 +2233,9 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
     if (run >= SERIAL_RUN) break;
     if (spec_block > 0 && lo >= spec_block) break;  // the cascade that stopped the speculative engine is done
     if (pops >= cool_lim) break;  // its cooldown is over
+    // the speculative engine is being allocated (first entry into this regime): return soon, so
+    // that the launches that carry it take the regime over
+    if (ws.spec_lazy && pops >= 4096) break;
     if (lo != ring_l || h >= ring_h0 + ring_n) {  // the bucket's next 64 slots, one load per lane
       ring_l = lo;
       ring_h0 = h;
@@ -2047,6 +2329,8 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
   __shared__ int s_ser;  // 1: the interrupt-dense regime, tiny batches popped serially
   __shared__ int s_specgo, s_specblk;  // hand the regime to the speculative engine; its resume level
   __shared__ int s_specool;            // regime entries to skip first (SpecCtl.cool)
+  __shared__ int s_lazyx;              // leave the launch: the speculative engine is being allocated
+  __shared__ int s_serx;               // leave the launch: serial pops in k_serial (mode 4)
   __shared__ Batch s_B;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const int Wt = ws.Wt;
@@ -2056,6 +2340,8 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     s_wcap = ctl->wcap;
     s_ser = 0;
     s_specgo = 0;
+    s_lazyx = 0;
+    s_serx = 0;
     s_specblk = ws.scl ? ctl->spec.block : -1;  // -1: engine off
     s_specool = ctl->spec.cool;
   }
@@ -2079,18 +2365,36 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
         long long c4[4] = {0, 0, 0, 0};
         if (s_ser && s_specblk >= 0 && s_specool <= 0 && lowest_bucket(s_head, s_tail, 0) >= s_specblk) {
           if (lane == 0) s_specgo = 1;  // interrupt-dense: speculative generations from here on
+        } else if (s_ser && ws.serk) {
+          // the serial-pop regime runs in k_serial (LDS-cached state, launched by the host when
+          // the progress mirror shows mode 4): hand the queue state over
+          if (ws.spec_lazy && lane == 0) ctl->spec_want = 1;  // the host allocates the engine
+          if (lane == 0) s_serx = 1;
         } else if (s_ser) {
           if (ws.spec_lazy && lane == 0) ctl->spec_want = 1;  // the host allocates the engine
+          const unsigned long long t0 = ws.diag ? __builtin_amdgcn_s_memrealtime() : 0;
           serial_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, c4,
                       s_specblk > 0 ? s_specblk : 0, s_specblk >= 0 ? &s_specool : nullptr);
+          if (ws.spec_lazy && lane == 0) s_lazyx = 1;
+          if (ws.diag && lane == 0) {
+            atomicAdd(&ws.diag[19], (unsigned long long)c4[0]);
+            atomicAdd(&ws.diag[20], __builtin_amdgcn_s_memrealtime() - t0);
+          }
           wave_sync();
           // the cascade that stopped the speculative engine is done, or its cooldown is over:
           // hand the regime back to it (not to a whole-bucket batch the next interrupt cuts again)
           if (s_specblk >= 0 && s_specool <= 0 && s_B.n > 0 && lowest_bucket(s_head, s_tail, 0) >= s_specblk &&
               lane == 0)
             s_specgo = 1;
-        } else
+        } else {
+          const unsigned long long t0 = ws.diag ? __builtin_amdgcn_s_memrealtime() : 0;
           tiny_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, s_wcnt[0], &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, c4);
+          if (ws.diag && lane == 0) {
+            atomicAdd(&ws.diag[16], (unsigned long long)c4[3]);
+            atomicAdd(&ws.diag[17], (unsigned long long)c4[0]);
+            atomicAdd(&ws.diag[18], __builtin_amdgcn_s_memrealtime() - t0);
+          }
+        }
         if (tid == 0) {
           nb_pops += c4[0];
           nb_items += c4[1];
@@ -2099,7 +2403,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
         }
       }
       __syncthreads();
-      if (s_specgo) break;
+      if (s_specgo || s_lazyx || s_serx) break;
       continue;
     }
     for (int k = tid; k < B.n; k += 1024) s_lab[k] = 0;
@@ -2239,6 +2543,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
       nb_items += B.n;
       nb_push += npush;
       s_wcap = next_wcap(s_wcap, B.n, ncommit, s_cut != NONE && ncommit == s_cut + 1);
+      if (ws.diag) atomicAdd(&ws.diag[23], (unsigned long long)ncommit);
     }
     __syncthreads();
     form_batch(s_qbase, s_head, s_tail, s_minpush, s_wcap, s_seg, &s_nseg, &s_n);
@@ -2287,6 +2592,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
       ctl->spec.on = 1;
       ctl->spec.block = 0;
     }
+    if (s_serx) nb.mode = 4;  // serial pops pending: only k_serial acts on this batch
     ctl->bat = nb;
     ctl->wcap = s_wcap;
     ctl->spec.cool = s_specool;
@@ -2299,6 +2605,362 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     ctl->pushes += nb_push;
     if (s_err) ctl->error |= s_err;
     if (s_B.n == 0 && !s_err) ctl->done = 1;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_serial: the serial-pop regime (see serial_loop) as a kernel of its own, one wave, launched by
+// the host when the progress mirror reports a batch in mode 4 ("serial pops pending", set by
+// k_scan's small-batch loop where it used to pop serially itself).  The same scalar program as
+// serial_loop -- pop the oldest item of the lowest non-empty bucket, fold its labelled
+// neighbours, push its unknown ones in L,R,T,B order -- but the flood state it touches lives in
+// an LDS cache: 2-way set-associative lines of 32 tiled entries (a tile pair, 8 x 4 pixels),
+// states and weights, written back on eviction and at exit (only the entries the loop wrote: a
+// dirty mask per line).  Nothing else touches the flood state while it runs (one kernel at a time
+// on the flood's stream), so the cache needs no coherence.  A pop reads its own line and at most
+// one horizontal and one vertical neighbour line; when all three fall into one set, the third is
+// read and written in global memory directly.  Queue slots stay in global memory (written
+// through; the popped bucket's next 64 slots are prefetched as in serial_loop).  The whole wave
+// runs one uniform program (uniform LDS addresses broadcast); only line fills and write-backs use
+// the lanes separately.
+constexpr int SER_WAYS = 4, SER_SETS = 128, SER_LINES = SER_WAYS * SER_SETS;
+constexpr int SER_RING = 16;  // per-bucket LDS ring of the pixels this launch pushed (queue slots)
+struct SerCache {
+  int st[SER_LINES][32];
+  unsigned w4[SER_LINES][32];
+  int tag[SER_LINES];       // line id (margin-relative tiled index >> 5), -1 empty; set s = ways 4s..4s+3
+  unsigned dirty[SER_LINES];
+  int rr[SER_SETS];         // next way to evict (round robin, skipping the pop's pinned lines)
+};
+
+__device__ __forceinline__ int ser_set(int L) { return (int)(((unsigned)L * 2654435761u) >> 25); }
+// every value the whole wave computes alike is moved to a scalar register, so the pop's control
+// flow is scalar (no exec-mask bookkeeping around uniform branches)
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Line L resident in the cache, never evicting lines pa / pb (4 ways: a pop pins at most 3):
+// its slot.  The fill's load is issued before the victim's write-back, so the load's wait
+// (vmcnt, in issue order) does not cover those stores.
+__device__ __forceinline__ int ser_line(SerCache& C, int* mkb, const unsigned* w4b, int L, int pa, int pb,
+                                        long long& fills) {
+  const int set = ser_set(L), s0 = SER_WAYS * set;
+  const int t0 = uni(C.tag[s0]), t1 = uni(C.tag[s0 + 1]), t2 = uni(C.tag[s0 + 2]), t3 = uni(C.tag[s0 + 3]);
+  if (t0 == L) return s0;
+  if (t1 == L) return s0 + 1;
+  if (t2 == L) return s0 + 2;
+  if (t3 == L) return s0 + 3;
+  int way = uni(C.rr[set]), tv = 0;
+#pragma unroll
+  for (int k = 0; k < SER_WAYS; ++k) {  // the first unpinned way from the round-robin pointer
+    tv = (way == 0) ? t0 : (way == 1) ? t1 : (way == 2) ? t2 : t3;
+    if (tv < 0 || (tv != pa && tv != pb)) break;
+    way = (way + 1) & (SER_WAYS - 1);
+  }
+  const int slot = s0 + way, lane = lane_id(), e = lane & 31;
+  // lanes 0-31 the line's states, 32-63 its weights: per-lane addresses, no branches
+  const int* src = (lane < 32) ? (mkb + L * 32 + e) : (const int*)(w4b + L * 32 + e);
+  const int v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (tv >= 0) {  // write back the victim's written entries
+    const unsigned dm = uni((int)C.dirty[slot]);
+    const int old = C.st[slot][e];
+    if (lane < 32 && ((dm >> e) & 1u)) mkb[tv * 32 + e] = old;
+  }
+  int* dst = (lane < 32) ? &C.st[slot][e] : (int*)&C.w4[slot][e];
+  *dst = v;
+  if (lane == 0) {
+    C.tag[slot] = L;
+    C.dirty[slot] = 0u;
+    C.rr[set] = (way + 1) & (SER_WAYS - 1);
+  }
+  ++fills;
+  return slot;
+}
+
+// every line's written entries back to global memory, two lines per step; the cache emptied
+__device__ void ser_flush(SerCache& C, int* mkb) {
+  const int lane = lane_id();
+  for (int k = 0; k < SER_LINES; k += 2) {
+    const int slot = k + (lane >> 5), e = lane & 31;
+    const int tg = C.tag[slot];
+    if (tg >= 0 && ((C.dirty[slot] >> e) & 1u)) mkb[tg * 32 + e] = C.st[slot][e];
+  }
+  wave_sync();
+  for (int k = lane; k < SER_LINES; k += 64) {
+    C.tag[k] = -1;
+    C.dirty[k] = 0u;
+  }
+  wave_sync();
+}
+
+// The pop loop of k_serial.  CACHED: the flood state through the LDS cache; otherwise straight
+// from global memory (serial_loop's accesses).  The popped bucket's next 64 queue slots are
+// prefetched into LDS, slots this launch pushed come from the per-bucket LDS rings, so a pop's
+// only global loads are line fills and prefetches.  Returns true when the cached loop gave the
+// cache up (more than 700 fills per 1024 pops): the caller flushes it and runs the rest uncached.
+struct SerRun {
+  int lo = NQ, run = 0, ring_l = -1, ring_h0 = 0, ring_n = 0;
+  long long pops = 0, pushes = 0, fills = 0;
+};
+
+template <bool CACHED>
+__device__ __forceinline__ bool ser_pops(const Ws& ws, SerCache& C, const int* s_qbase, int* s_head,
+                                                   int* s_tail, const int* s_bent, int (*s_bring)[SER_RING],
+                                                   int* s_ring, int* s_err, SerRun& R, int spec_block,
+                                                   long long cool_lim) {
+  const int lane = lane_id();
+  const int Wt = ws.Wt, marg = ws.marg;
+  int* const mkb = ws.mk - marg;
+  const unsigned* const w4b = (const unsigned*)(ws.w4 - marg);
+  int lo = R.lo, run = R.run, ring_l = R.ring_l, ring_h0 = R.ring_h0, ring_n = R.ring_n;
+  long long pops = R.pops, pushes = R.pushes, fills = R.fills, fills0 = R.fills;
+  bool dropped = false;
+  while (lo < NQ) {
+    const int h = uni(s_head[lo]), tl = uni(s_tail[lo]), navail = tl - h;
+    if (navail <= 0) {
+      lo = lowest_bucket(s_head, s_tail, lo + 1);
+      continue;
+    }
+    if (run >= SERIAL_RUN) break;
+    if (spec_block > 0 && lo >= spec_block) break;  // the cascade that stopped the speculative engine is done
+    if (pops >= cool_lim) break;                    // its cooldown is over
+    if (ws.spec_lazy && pops >= 4096) break;        // the engine is being allocated: let it take over
+    int p;
+    if (h >= uni(s_bent[lo]) && h >= tl - SER_RING) {  // pushed by this launch: its LDS ring
+      p = uni(s_bring[lo][h & (SER_RING - 1)]);
+    } else {
+      if (lo != ring_l || h >= ring_h0 + ring_n) {  // the bucket's next 64 slots, one load per lane
+        ring_l = lo;
+        ring_h0 = h;
+        ring_n = min(navail, 64);
+        const int v = (lane < ring_n) ? ld_qbuf_v(ws, s_qbase[lo] + h + lane) : 0;
+        s_ring[lane] = v;
+      }
+      p = uni(s_ring[h - ring_h0]);
+    }
+    const int pb = p + marg;
+    int nv[4], st[4], sl[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) nv[d] = nbi(pb, d, Wt);
+    unsigned w4;
+    int s0 = -1;
+    if (CACHED) {
+      const int L0 = pb >> 5;
+      s0 = ser_line(C, mkb, w4b, L0, -1, -1, fills);
+      int Lh = -1, sh = -1;  // the horizontal neighbour line (left or right: one at most)
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const int L = nv[d] >> 5;
+        if (L != L0) {
+          Lh = L;
+          sh = ser_line(C, mkb, w4b, L, L0, -1, fills);
+        }
+      }
+      int sv = -1;  // the vertical one (up or down)
+#pragma unroll
+      for (int d = 2; d < 4; ++d) {
+        const int L = nv[d] >> 5;
+        if (L != L0 && L != Lh) sv = ser_line(C, mkb, w4b, L, L0, Lh, fills);
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int L = nv[d] >> 5;
+        sl[d] = (L == L0) ? s0 : (L == Lh) ? sh : sv;
+        st[d] = uni(C.st[sl[d]][nv[d] & 31]);
+      }
+      w4 = (unsigned)uni((int)C.w4[s0][pb & 31]);
+    } else {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        sl[d] = -1;
+        st[d] = uni(__hip_atomic_load(mkb + nv[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      }
+      w4 = (unsigned)uni((int)w4b[pb]);
+    }
+    int lab = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      if (st[d] > 0) lab = fold_lab(lab, st[d]);
+    if (lab == 0) {  // impossible for an exact queue
+      *s_err = ERR_STATE;
+      lab = WSHED;
+    }
+    if (CACHED) {
+      C.st[s0][pb & 31] = lab;
+      C.dirty[s0] |= 1u << (pb & 31);
+    } else {
+      mkb[pb] = lab;
+    }
+    s_head[lo] = h + 1;
+    ++pops;
+    bool lower = false;
+    int newlo = lo;
+    if (lab != WSHED) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        if (st[d] != 0) continue;
+        const int t = (int)((w4 >> (8 * d)) & 255u);
+        const int tt = uni(s_tail[t]);
+        const int dest = s_qbase[t] + tt;
+        if (dest < 0 || (long long)dest >= ws.qcap) {
+          *s_err = ERR_CAPACITY;
+          continue;
+        }
+        ws.qbuf[dest] = nv[d] - marg;
+        s_bring[t][tt & (SER_RING - 1)] = nv[d] - marg;
+        if (CACHED) {
+          C.st[sl[d]][nv[d] & 31] = queued_state(dest);
+          C.dirty[sl[d]] |= 1u << (nv[d] & 31);
+        } else {
+          mkb[nv[d]] = queued_state(dest);
+        }
+        s_tail[t] = tt + 1;
+        ++pushes;
+        if (t < lo) lower = true;
+        newlo = min(newlo, t);
+      }
+    }
+    run = lower ? 0 : run + 1;
+    lo = newlo;
+    if (*s_err) break;
+    // a cache that misses on most pops (uniform-random frames: the flood front is everywhere at
+    // once) costs more than it saves: judged every 1024 pops
+    if (CACHED && (pops & 1023) == 0) {
+      if (fills - fills0 > 700) {
+        dropped = true;
+        break;
+      }
+      fills0 = fills;
+    }
+  }
+  R.lo = lo;
+  R.run = run;
+  R.ring_l = ring_l;
+  R.ring_h0 = ring_h0;
+  R.ring_n = ring_n;
+  R.pops = pops;
+  R.pushes = pushes;
+  R.fills = fills;
+  return dropped;
+}
+
+__global__ __launch_bounds__(64) void k_serial(Ws ws, int iter) {
+  Ctl* ctl = ws.ctl;
+  __shared__ SerCache C;
+  __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ];
+  __shared__ int s_bent[NQ];               // bucket tails at entry: later slots were pushed here
+  __shared__ int s_bring[NQ][SER_RING];    // the last SER_RING pixels pushed to each bucket
+  __shared__ Seg s_seg[NQ];
+  __shared__ int s_ring[64];               // the next 64 queue slots of one bucket (prefetched)
+  __shared__ int s_err, s_nseg, s_n, s_specool, s_specblk;
+  const int lane = lane_id();
+  const Batch B0 = ctl->bat;
+  if (B0.mode == 4 && !ctl->error) {
+    for (int k = lane; k < NQ; k += 64) {
+      s_qbase[k] = ctl->qbase[k];
+      s_head[k] = ctl->qhead[k];
+      s_tail[k] = ctl->qtail[k];
+      s_bent[k] = s_tail[k];
+    }
+    for (int k = lane; k < SER_SETS; k += 64) C.rr[k] = 0;
+    for (int k = lane; k < SER_LINES; k += 64) {
+      C.tag[k] = -1;
+      C.dirty[k] = 0u;
+    }
+    if (lane == 0) {
+      s_err = 0;
+      s_specblk = ws.scl ? ctl->spec.block : -1;  // -1: engine off
+      s_specool = ctl->spec.cool;
+    }
+    wave_sync();
+    int* const mkb = ws.mk - ws.marg;
+    const int spec_block = s_specblk > 0 ? s_specblk : 0;
+    const long long cool_lim = (s_specblk >= 0 && s_specool > 0) ? s_specool : (1ll << 62);
+    SerRun R;
+    R.lo = lowest_bucket(s_head, s_tail, 0);
+    const unsigned long long t_start = ws.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+    // the cached loop, then -- if the cache kept missing -- the rest of the run without it
+    const bool dropped = ser_pops<true>(ws, C, s_qbase, s_head, s_tail, s_bent, s_bring, s_ring, &s_err, R,
+                                        spec_block, cool_lim);
+    if (dropped) {
+      ser_flush(C, mkb);
+      ser_pops<false>(ws, C, s_qbase, s_head, s_tail, s_bent, s_bring, s_ring, &s_err, R, spec_block, cool_lim);
+    } else {
+      ser_flush(C, mkb);
+    }
+    const long long pops = R.pops, pushes = R.pushes, fills = R.fills;
+    if (ws.diag && lane == 0) {
+      atomicAdd(&ws.diag[19], (unsigned long long)pops);
+      atomicAdd(&ws.diag[20], __builtin_amdgcn_s_memrealtime() - t_start);
+      atomicAdd(&ws.diag[21], 1ull);
+      atomicAdd(&ws.diag[22], (unsigned long long)fills);
+    }
+    wave_sync();
+    form_batch(s_qbase, s_head, s_tail, 0, 0, s_seg, &s_nseg, &s_n);
+    wave_sync();
+    const int ns = s_nseg;
+    if (s_specblk >= 0 && s_specool > 0 && lane == 0) s_specool = (int)max(0ll, (long long)s_specool - pops);
+    wave_sync();
+    // the cascade that stopped the speculative engine is done, or its cooldown is over: hand the
+    // regime back to it (as small_loop does after serial_loop)
+    const bool specgo = s_specblk >= 0 && s_specool <= 0 && ns > 0 && lowest_bucket(s_head, s_tail, 0) >= s_specblk;
+    for (int k = lane; k < NQ; k += 64) {
+      ctl->qhead[k] = s_head[k];
+      ctl->qtail[k] = s_tail[k];
+    }
+    for (int k = lane; k < ns; k += 64) ctl->seg[k] = s_seg[k];
+    int q = 0;
+#pragma unroll
+    for (int k = 0; k < NQ / 64; ++k) q += s_tail[lane + 64 * k] - s_head[lane + 64 * k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    if (lane == 0) {
+      Batch nb;
+      nb.mode = 0;
+      nb.epoch = B0.epoch + 1;
+      nb.ncommit = 0;
+      nb.nchunk = 0;
+      nb.rrun = 0;
+      nb.nseg = ns;
+      nb.n = (ns > 0) ? s_n : 0;
+      nb.L = (ns > 0) ? s_seg[0].L : -1;
+      nb.bstart = (ns > 0) ? s_seg[0].bstart : 0;
+      if (specgo) {
+        spec_begin(ctl, nb, nb.L, s_qbase[nb.L] + s_head[nb.L], s_tail[nb.L] - s_head[nb.L]);
+        if (ctl->spec.fresh || ctl->spec.tstart == 0) {  // flood start, or after a cooldown: judge anew
+          ctl->spec.fresh = 0;
+          ctl->spec.accg = 0;
+          ctl->spec.tstart = (long long)__builtin_amdgcn_s_memrealtime();
+          ctl->spec.pstart = ctl->pops + pops;
+        }
+        ctl->spec.on = 1;
+        ctl->spec.block = 0;
+      }
+      ctl->bat = nb;
+      ctl->wcap = 0;  // the next batch: a whole generation (next_wcap shrinks it again on a cut)
+      if (s_specblk >= 0) ctl->spec.cool = s_specool;
+      ctl->cut = NONE;
+      ctl->segcut = NONE;
+      ctl->minpush = NQ;
+      ctl->remaining = q;
+      ctl->batches += pops;
+      ctl->pops += pops;
+      ctl->items += pops;
+      ctl->pushes += pushes;
+      if (s_err) ctl->error |= s_err;
+      if (nb.n == 0 && !s_err) ctl->done = 1;
+    }
+  }
+  wave_sync();
+  if (lane == 0 && ws.hmir) {
+    const Batch nb = ctl->bat;
+    __hip_atomic_store(ws.hmir + 1, ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 2, ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 3, ctl->remaining, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 4, ctl->spec.on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 5, ctl->spec_want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 6, fast_batch(nb) ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 7, nb.mode == 4 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

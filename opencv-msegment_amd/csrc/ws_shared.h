@@ -22,6 +22,8 @@ constexpr int SMALL_MAX = 4096;    // batches up to this size run in k_scan's on
 constexpr int PAL_LDS_MAX = 16384; // palettes up to this many labels are staged in LDS
 constexpr int MERGE_CAP = 1 << 22; // largest multi-segment batch (items)
 constexpr int WMIN = 64;           // smallest batch window (one wave: the tiny-batch loop)
+constexpr int FAST_CH = 120;       // k_commit_fast: batches of at most FAST_CH chunks of CH items
+                                   // (4 FAST_CH + 1 blocks of 1024 threads: resident at 2 per CU)
 // Batch window after committing ncommit of n items: an interrupt cut (a push below the item's
 // level) means the queue order is turning over fast, so the next batch is a short prefix; a
 // batch that filled its window uncut quadruples it.  Prefixes of the queue order: exact.
@@ -135,7 +137,8 @@ struct Batch {
   unsigned epoch;  // tag of this batch's tl granules
   int ncommit;     // committed prefix (set by k_scan)
   int nchunk;      // chunks of the committed prefix (set by k_scan)
-  int mode;        // 0 = flood batch, 1 = phase-1 pseudo-batch (items = ilist)
+  int mode;        // 0 = flood batch, 1 = phase-1 pseudo-batch (items = ilist), 3 = speculative
+                   // generation, 4 = serial pops pending (k_serial)
   int rrun;        // k_resolve re-runs of this batch so far (chunks given up: see k_resolve)
 };
 
@@ -163,7 +166,9 @@ struct Ctl {
   SpecCtl spec;
   int spec_want;     // the serial regime was entered while the speculative engine was enabled but
                      // its workspace not yet allocated (Ws.spec_lazy): the host allocates it
-  int pad2;
+  unsigned hold;     // epoch of a decided batch k_commit_fast declined (k_resolve must not re-run it)
+  int pad3;
+  unsigned farrive[8];  // k_commit_fast: sub-round blocks done reading, by blockIdx % 8 (zeroed after)
 };
 
 static_assert(__builtin_offsetof(Ctl, error) % 8 == 0 && __builtin_offsetof(Ctl, rgive) == __builtin_offsetof(Ctl, error) + 4,
@@ -186,7 +191,8 @@ struct Ws {
   unsigned long long* cflag;  // per k_resolve chunk: {epoch, run} of its claim, epoch of its completion
   Ctl* ctl;
   unsigned long long* diag;  // nullptr = off; else 8 counters (msg_set_diag)
-  int* hmir;         // host-mapped progress mirror {iteration, done, error, remaining, spec, spec_want} (k_scatter)
+  int* hmir;         // host-mapped progress mirror {iteration, done, error, remaining, spec, spec_want,
+                     // fast batch, serial pending}
   // speculative generations (nullptr when the engine is off); claims and labels are indexed by
   // tiled pixel like mk, one array of snp entries per round parity
   unsigned long long* scl;   // 2 x snp round claims {tag, rank, popped}
@@ -202,6 +208,7 @@ struct Ws {
   long long snp;
   long long slogcap;
   int spec_lazy;     // 1: engine enabled, workspace not allocated yet (k_scan reports spec_want)
+  int serk;          // 1: the serial-pop regime runs in k_serial (mode 4), 0: inside k_scan
   int H, W;
   int Wt;            // tiles per tile row = ceil(W / 4)
   int marg;          // tiled entries of margin before mk / w4 (mk - marg starts the state array)

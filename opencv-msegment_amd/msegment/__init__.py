@@ -120,8 +120,17 @@ class Segmenter:
         return out
 
     def set_diag(self, on=True):
-        """In-kernel counters; on=2 also injects k_resolve give-ups (tests of the re-run path)."""
-        self._check(self._L.msg_set_diag(self._h, 2 if on == 2 else (1 if on else 0)))
+        """In-kernel counters; on=2 also injects k_resolve give-ups (tests of the re-run path);
+        on=3 reports the one-workgroup loop's regime split instead (msegment.h, msg_set_diag)."""
+        self._check(self._L.msg_set_diag(self._h, int(on) if on in (2, 3) else (1 if on else 0)))
+
+    def set_fast_commit(self, on=True):
+        """Two-launch iterations for large flood batches (default on); off = three launches."""
+        self._check(self._L.msg_set_fast_commit(self._h, 1 if on else 0))
+
+    def set_serial_kernel(self, on=True):
+        """Serial-pop regime in k_serial with LDS-cached state (default off: inside k_scan)."""
+        self._check(self._L.msg_set_serial_kernel(self._h, 1 if on else 0))
 
     def set_speculative(self, on=True):
         """Speculative generations for the interrupt-dense regime (default on); off = serial pops."""

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Focused GPU pass: named pytest selection (-k EXPR) then one bench line.  usage: scripts/gpu_focus.sh <tag> <-k expr> [bench args]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-focus}; K=${2:-fast}; shift 2 || true
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -k "$K" --timeout 240 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -n 5 "$OUT/pytest_gpu.log"
+case $rc in 0|1|5) ;; *) echo "STOP"; exit $rc ;; esac
+timeout -k 10 600 python bench.py "$@" > "$OUT/bench.log" 2>&1
+rc=$?; echo "bench rc=$rc"; tail -n 3 "$OUT/bench.log" | cut -c1-3000

@@ -542,3 +542,39 @@ def test_prep_paths_on_misaligned_device_buffers(seg, W):
         torch.cuda.synchronize()
         outs.append(lab.cpu().numpy())
     assert np.array_equal(outs[0], want) and np.array_equal(outs[1], want)
+
+
+@pytest.mark.parametrize("kind,S,seed", [("mosaic", 2048, 5), ("mosaic", 1024, 1), ("mosaic_noise", 512, 9)])
+def test_fast_commit_matches_three_launch_iterations(seg, kind, S, seed):
+    """k_commit_fast (two-launch iterations for batches of 4 K..256 K items) against the three-launch
+    iterations and the oracle; the fast path must actually have run on the mosaic frames."""
+    img, m, _ = synth.frame(kind, S, S, seed)
+    want = ws_oracle.watershed(img, m)
+    seg.set_profiling(True)
+    try:
+        seg.kernel_profile(reset=True)
+        fast = gpu_ws(seg, img, m)
+        prof = seg.kernel_profile(reset=True)
+        seg.set_fast_commit(False)
+        slow = gpu_ws(seg, img, m)
+        prof_off = seg.kernel_profile(reset=True)
+    finally:
+        seg.set_fast_commit(True)
+        seg.set_profiling(False)
+    assert np.array_equal(fast, want) and np.array_equal(slow, want)
+    assert prof_off.get("k_commit_fast", (0, 0))[0] == 0
+    if kind == "mosaic":
+        assert prof["k_commit_fast"][0] > 0
+
+
+def test_fast_commit_with_give_ups(seg):
+    """Injected k_resolve give-ups (msg_set_diag 2): k_commit_fast must schedule the re-run instead
+    of committing; then the same context without injection."""
+    img, m, _ = synth.frame("mosaic", 1024, 1024, 3)
+    want = ws_oracle.watershed(img, m)
+    seg.set_diag(2)
+    try:
+        assert np.array_equal(gpu_ws(seg, img, m), want)
+    finally:
+        seg.set_diag(False)
+    assert np.array_equal(gpu_ws(seg, img, m), want)
