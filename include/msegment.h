@@ -82,7 +82,11 @@ typedef struct msg_kernel_profile {
 } msg_kernel_profile;
 
 /* One context per thread: owns a HIP stream and the device workspace on `device_ordinal`.
- * flags: reserved, pass 0.  Replaces: OpenCV.loadLocally()  App.java:15 (library bring-up). */
+ * flags: 0, or MSG_CREATE_HIGH_PRIORITY for a high-priority stream (the batch entry points'
+ * internal sub-contexts use it: the HIP runtime keeps streams of different priorities on
+ * different hardware queues, so concurrent floods overlap even at GPU_MAX_HW_QUEUES=4).
+ * Replaces: OpenCV.loadLocally()  App.java:15 (library bring-up). */
+#define MSG_CREATE_HIGH_PRIORITY 0x1u
 int  msg_create(msg_ctx** out, int device_ordinal, unsigned flags);
 void msg_destroy(msg_ctx* ctx);
 const char* msg_last_error(const msg_ctx* ctx);

@@ -52,9 +52,9 @@ struct msg_ctx {
   bool serk = false;            // msg_set_serial_kernel: serial pops in k_serial (LDS-cached state)
   bool spec = true;             // msg_set_speculative
   long long spec_np = 0, spec_logcap = 0;
-  unsigned long long *d_scl = nullptr, *d_sfin = nullptr, *d_stl = nullptr, *d_slog = nullptr;
+  SpecPx* d_spx = nullptr;       // per tiled pixel: both parities' claims and labels, final claim
+  unsigned long long *d_stl = nullptr, *d_slog = nullptr;
   unsigned long long *d_ssig = nullptr, *d_stmp = nullptr, *d_sflag = nullptr;
-  int32_t* d_slab = nullptr;
   int4* d_srec = nullptr;
   int2* d_sfrec = nullptr;
   unsigned stag = 0;            // last round tag used (claims carry it; never reused)
@@ -232,8 +232,8 @@ void free_flood(msg_ctx* c) {
 }
 
 void free_spec(msg_ctx* c) {
-  dfree(c->d_scl); dfree(c->d_sfin); dfree(c->d_stl); dfree(c->d_slog); dfree(c->d_ssig);
-  dfree(c->d_stmp); dfree(c->d_sflag); dfree(c->d_slab); dfree(c->d_srec); dfree(c->d_sfrec);
+  dfree(c->d_spx); dfree(c->d_stl); dfree(c->d_slog); dfree(c->d_ssig);
+  dfree(c->d_stmp); dfree(c->d_sflag); dfree(c->d_srec); dfree(c->d_sfrec);
   c->spec_np = c->spec_logcap = 0;
   c->stag = 0;
 }
@@ -248,9 +248,7 @@ int ensure_spec(msg_ctx* c, long long np, long long n, hipStream_t st) {
   if (np > c->spec_np || logcap > c->spec_logcap) {
     free_spec(c);
     const long long slots = (long long)c->spec_grid * SPEC_BS;
-    HIPCHK(c, hipMalloc((void**)&c->d_scl, np * 2 * 8));
-    HIPCHK(c, hipMalloc((void**)&c->d_sfin, np * 8));
-    HIPCHK(c, hipMalloc((void**)&c->d_slab, np * 2 * 4));
+    HIPCHK(c, hipMalloc((void**)&c->d_spx, np * sizeof(SpecPx)));
     HIPCHK(c, hipMalloc((void**)&c->d_stl, (size_t)SPEC_WIN * 8));
     HIPCHK(c, hipMalloc((void**)&c->d_slog, logcap * 8));
     HIPCHK(c, hipMalloc((void**)&c->d_srec, (size_t)2 * SPEC_WIN * sizeof(int4)));
@@ -261,8 +259,7 @@ int ensure_spec(msg_ctx* c, long long np, long long n, hipStream_t st) {
     c->spec_np = np;
     c->spec_logcap = logcap;
   }
-  HIPCHK(c, hipMemsetAsync(c->d_scl, 0, c->spec_np * 2 * 8, st));
-  HIPCHK(c, hipMemsetAsync(c->d_sfin, 0, c->spec_np * 8, st));
+  HIPCHK(c, hipMemsetAsync(c->d_spx, 0, c->spec_np * sizeof(SpecPx), st));
   HIPCHK(c, hipMemsetAsync(c->d_stl, 0, (size_t)SPEC_WIN * 8, st));
   HIPCHK(c, hipMemsetAsync(c->d_sflag, 0, (size_t)(SPEC_WIN / SPEC_FT + 2) * 8, st));
   c->stag = 0;
@@ -417,8 +414,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   const long long ntiled = (long long)((H + 3) / 4) * ws.Wt * 16;
   const bool spec = c->spec && ntiled <= (1ll << 28) && H >= 3 && W >= 3;
   auto bind_spec = [&](bool on) {
-    ws.scl = on ? c->d_scl : nullptr; ws.sfin = on ? c->d_sfin : nullptr;
-    ws.slab = on ? c->d_slab : nullptr; ws.stl = on ? c->d_stl : nullptr;
+    ws.spx = on ? c->d_spx : nullptr; ws.stl = on ? c->d_stl : nullptr;
     ws.slog = on ? c->d_slog : nullptr; ws.srec = on ? c->d_srec : nullptr;
     ws.ssig = on ? c->d_ssig : nullptr; ws.sfrec = on ? c->d_sfrec : nullptr;
     ws.stmp = on ? c->d_stmp : nullptr; ws.sflag = on ? c->d_sflag : nullptr;
@@ -605,7 +601,7 @@ constexpr int MAX_INFLIGHT = 8;
 int ensure_subs(msg_ctx* c, int k) {
   while ((int)c->subs.size() < k) {
     msg_ctx* sub = nullptr;
-    const int rc = msg_create(&sub, c->dev, 0);
+    const int rc = msg_create(&sub, c->dev, MSG_CREATE_HIGH_PRIORITY);
     if (rc) return fail(c, rc, "batch sub-context creation failed (%d)", rc);
     c->subs.push_back(sub);
   }
@@ -832,8 +828,7 @@ extern "C" {
 int msg_abi_version(void) { return MSG_ABI_VERSION; }
 
 int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
-  (void)flags;
-  if (!out) return MSG_EINVAL;
+  if (!out || (flags & ~MSG_CREATE_HIGH_PRIORITY)) return MSG_EINVAL;
   *out = nullptr;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MSG_EHIP;
@@ -841,7 +836,18 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
   msg_ctx* c = new (std::nothrow) msg_ctx();
   if (!c) return MSG_ENOMEM;
   c->dev = device_ordinal;
-  if (hipSetDevice(c->dev) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
+  // MSEG_STREAM_PRIORITY=high|low: the context's stream at that priority (a tuning knob for
+  // concurrent floods: the HIP runtime keeps streams of different priorities on different
+  // hardware queues)
+  int prio = 0;
+  {
+    const char* e = getenv("MSEG_STREAM_PRIORITY");
+    int lo = 0, hi = 0;
+    if ((e || (flags & MSG_CREATE_HIGH_PRIORITY)) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+      prio = (e && e[0] == 'l') ? lo : (e && e[0] == 'd') ? 0 : hi;
+  }
+  if (hipSetDevice(c->dev) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->own, hipStreamNonBlocking, prio) != hipSuccess ||
       hipMalloc((void**)&c->d_ctl, sizeof(Ctl)) != hipSuccess ||
       hipHostMalloc((void**)&c->h_mir, 8 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||

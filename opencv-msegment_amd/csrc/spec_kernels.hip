@@ -77,30 +77,43 @@ __device__ __forceinline__ unsigned long long smix(unsigned long long h, unsigne
 }
 
 struct SpecView {
-  const unsigned long long* cur;   // this round's claims
-  const unsigned long long* prev;  // the previous round's (valid when hasprev)
-  const unsigned long long* fin;
-  const int32_t* slc;
-  const int32_t* slp;
+  const SpecPx* spx;
+  int par;          // this round's parity (T & 1): cl[par], lab[par]; the previous round's 1 - par
   unsigned T, G;
   bool hasprev;
 };
 
+// A pixel's record and state as loaded for spec_decide: relaxed agent-scope loads (sc1, L2-served,
+// never a stale L1 line of words written inside this round) and no wait of their own, so a
+// cascade pop issues all four neighbours' loads before the first use (volatile loads would put
+// a full vmcnt(0) wait behind each one).
+struct SpecRec {
+  unsigned long long cl0, cl1, fin, labs;
+  int s;
+};
+__device__ __forceinline__ SpecRec spec_load(const Ws& ws, const SpecView& V, int z) {
+  SpecRec r;
+  r.cl0 = ld_ag64(&V.spx[z].cl[0]);
+  r.cl1 = ld_ag64(&V.spx[z].cl[1]);
+  r.fin = ld_ag64(&V.spx[z].fin);
+  r.labs = ld_ag64((const unsigned long long*)&V.spx[z].lab[0]);
+  r.s = ws.mk[z];
+  return r;
+}
+
 // State of pixel z as item j sees it: > 0 label, WSHED, 0 unknown, INQ queued or pushed.
 // Own writes first, then final items' writes, then the previous round's lower ranks, else the
 // pre-generation state.
-__device__ __forceinline__ int spec_view(const Ws& ws, const SpecView& V, int j, int z, bool own) {
-  // every word loaded up front (labels too, used or not): one memory round trip per view
-  const unsigned long long o = own ? ld_ag64(V.cur + z) : 0ull;
-  const int lc = own ? ld_ag32(V.slc + z) : 0;
-  const unsigned long long f = V.fin[z];  // promotes racing this load: prev covers them
-  const unsigned long long c = V.hasprev ? V.prev[z] : 0ull;
-  const int lp = V.hasprev ? V.slp[z] : 0;
-  const int s = ws.mk[z];
+__device__ __forceinline__ int spec_decide(const SpecView& V, const SpecRec& r, int j, bool own) {
+  const unsigned long long o = own ? (V.par ? r.cl1 : r.cl0) : 0ull;
+  const int lc = (int)(uint32_t)(V.par ? (r.labs >> 32) : r.labs);
+  const unsigned long long f = r.fin;
+  const unsigned long long c = V.hasprev ? (V.par ? r.cl0 : r.cl1) : 0ull;
+  const int lp = (int)(uint32_t)(V.par ? r.labs : (r.labs >> 32));
   if (own && sc_tag(o) == V.T && sc_rank(o) == j) return (o & 1ull) ? lc : INQ;
   if ((unsigned)(f >> 33) == V.G) return ((f >> 32) & 1ull) ? (int)(uint32_t)f : INQ;
   if (V.hasprev && sc_tag(c) == V.T - 1 && sc_rank(c) < j) return (c & 1ull) ? lp : INQ;
-  return (s >= WSHED) ? s : INQ;
+  return (r.s >= WSHED) ? r.s : INQ;
 }
 
 // top-pop granule of item k as item j may use it in round T: this round's, or a final item's
@@ -163,23 +176,21 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
   if (tid == 0) s_exec = 0;
   const unsigned T = ctl->spec.T, G = ctl->spec.G;
   const int P = ctl->spec.P, n = ctl->spec.n, L = ctl->spec.L, bstart = ctl->spec.bstart;
-  const long long np = ws.snp;
   const int par = (int)(T & 1u), ppar = (int)((T - 1u) & 1u);
   SpecView V;
-  V.cur = ws.scl + (size_t)par * np;
-  V.prev = ws.scl + (size_t)ppar * np;
-  V.fin = ws.sfin;
-  V.slc = ws.slab + (size_t)par * np;
-  V.slp = ws.slab + (size_t)ppar * np;
+  V.spx = ws.spx;
+  V.par = par;
   V.T = T;
   V.G = G;
   V.hasprev = T > G;
-  unsigned long long* const cur = ws.scl + (size_t)par * np;
-  int32_t* const slc = ws.slab + (size_t)par * np;
+  SpecPx* const spx = ws.spx;
   unsigned long long* const tmp = ws.stmp + (size_t)(blockIdx.x * SPEC_BS + tid) * SPEC_RL;
   const unsigned long long etag = (unsigned long long)T << 32;
   const int Wt = ws.Wt, marg = ws.marg;
   bool stop = false;
+#ifdef MSEG_SPEC_PROF
+  long long pf_n = 0, pf_q = 0, pf_sel = 0, pf_load = 0, pf_write = 0;  // cascade-pop phases (lane sums)
+#endif
   unsigned long long* const dg = ws.diag ? ws.diag + 8 : nullptr;  // msg_set_diag: the round's wall-clock split (10 ns ticks)
   const long long tk0 = dg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
   long long tw = 0, tc = 0;
@@ -200,10 +211,10 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
         const unsigned long long r = ws.slog[rc.x + k];
         const int y = (int)(r & 0x0fffffffu);
         const unsigned dm = (unsigned)(r >> 28) & 15u;
-        st_ag64(ws.sfin + y, fin_word(G, 1u, (int)(uint32_t)(r >> 32)));
+        st_ag64(&ws.spx[y].fin, fin_word(G, 1u, (int)(uint32_t)(r >> 32)));
 #pragma unroll
         for (int d = 0; d < 4; ++d)
-          if ((dm >> d) & 1u) st_ag64(ws.sfin + (nbi(y + marg, d, Wt) - marg), fin_word(G, 0u, 0));
+          if ((dm >> d) & 1u) st_ag64(&ws.spx[nbi(y + marg, d, Wt) - marg].fin, fin_word(G, 0u, 0));
       }
     }
     // ---- execute [P, n): gather the top pop ----
@@ -218,22 +229,21 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
       p = ws.qbuf[bstart + j];
       wp = (unsigned)ws.w4[p];
       const int pb = p + marg;
-      int s4[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) nbp[d] = nbi(pb, d, Wt) - marg;
+      SpecRec rr[4];  // all four records in flight before the first decision
+#pragma unroll
+      for (int d = 0; d < 4; ++d) rr[d] = spec_load(ws, V, nbp[d]);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        nbp[d] = nbi(pb, d, Wt) - marg;
-        s4[d] = ws.mk[nbp[d]];
-      }
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        if (s4[d] <= -3) {  // an earlier item of this generation: its top pop of this round
-          const int k = state_slot(s4[d]) - bstart;
+        if (rr[d].s <= -3) {  // an earlier item of this generation: its top pop of this round
+          const int k = state_slot(rr[d].s) - bstart;
           if (k >= 0 && k < j) {
             dep[d] = k;
             continue;
           }
         }
-        const int v = spec_view(ws, V, j, nbp[d], false);
+        const int v = spec_decide(V, rr[d], j, false);
         if (v > 0) base_lab = fold_lab(base_lab, v);
         else if (v == 0) zm |= 1u << d;
       }
@@ -341,8 +351,8 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
     int nrec = 0;
     if (ex) {
       // ---- the top pop's writes, then the cascade (levels < L, lowest first, FIFO) ----
-      claim_max(cur + p, spec_claim(T, j, 1u));
-      st_ag32(slc + p, mylab);
+      claim_max(&spx[p].cl[par], spec_claim(T, j, 1u));
+      st_ag32(&spx[p].lab[par], mylab);
       int nq = 0;
       unsigned dm = 0;
       if (mylab != WSHED) {
@@ -350,7 +360,7 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
         for (int d = 0; d < 4; ++d) {
           if (!((pm >> d) & 1u)) continue;
           const int z = nbp[d];
-          claim_max(cur + z, spec_claim(T, j, 0u));
+          claim_max(&spx[z].cl[par], spec_claim(T, j, 0u));
           const unsigned t = (wp >> (8 * d)) & 255u;
           if ((int)t < L) {
             if (nq < SPEC_QCAP) lq[(nq++) * SPEC_BS + tid] = ((unsigned long long)t << 32) | (unsigned)z;
@@ -369,6 +379,11 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
           ovf = cap = true;
           break;
         }
+#ifdef MSEG_SPEC_PROF
+        const long long q0 = (long long)__builtin_amdgcn_s_memtime();
+        pf_n += 1;
+        pf_q += nq;
+#endif
         int bi = 0;
         unsigned long long be = lq[tid];
         for (int k = 1; k < nq; ++k) {
@@ -381,30 +396,44 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
         for (int k = bi; k + 1 < nq; ++k) lq[k * SPEC_BS + tid] = lq[(k + 1) * SPEC_BS + tid];
         --nq;
         const int y = (int)(uint32_t)be;
+#ifdef MSEG_SPEC_PROF
+        const long long q1 = (long long)__builtin_amdgcn_s_memtime();
+        pf_sel += q1 - q0;
+#endif
         const unsigned wy = (unsigned)ws.w4[y];
         const int yb = y + marg;
         int nby[4], v[4];
   #pragma unroll
         for (int d = 0; d < 4; ++d) nby[d] = nbi(yb, d, Wt) - marg;
-  #pragma unroll
-        for (int d = 0; d < 4; ++d) v[d] = spec_view(ws, V, j, nby[d], true);
+        {  // four named records (an indexed array of them lands in scratch)
+          const SpecRec r0 = spec_load(ws, V, nby[0]), r1 = spec_load(ws, V, nby[1]);
+          const SpecRec r2 = spec_load(ws, V, nby[2]), r3 = spec_load(ws, V, nby[3]);
+          v[0] = spec_decide(V, r0, j, true);
+          v[1] = spec_decide(V, r1, j, true);
+          v[2] = spec_decide(V, r2, j, true);
+          v[3] = spec_decide(V, r3, j, true);
+        }
         int lab = 0;
   #pragma unroll
         for (int d = 0; d < 4; ++d)
           if (v[d] > 0) lab = fold_lab(lab, v[d]);
+#ifdef MSEG_SPEC_PROF
+        const long long q2 = (long long)__builtin_amdgcn_s_memtime();
+        pf_load += q2 - q1;
+#endif
         if (lab == 0) {  // own writes hidden by a conflicting lower rank: unstable
           ovf = true;
           lab = WSHED;
         }
-        claim_max(cur + y, spec_claim(T, j, 1u));
-        st_ag32(slc + y, lab);
+        claim_max(&spx[y].cl[par], spec_claim(T, j, 1u));
+        st_ag32(&spx[y].lab[par], lab);
         unsigned dmy = 0;
         if (lab != WSHED) {
   #pragma unroll
           for (int d = 0; d < 4; ++d) {
             if (v[d] != 0) continue;
             const int z = nby[d];
-            claim_max(cur + z, spec_claim(T, j, 0u));
+            claim_max(&spx[z].cl[par], spec_claim(T, j, 0u));
             const unsigned t = (wy >> (8 * d)) & 255u;
             if ((int)t < L) {
               if (nq < SPEC_QCAP) lq[(nq++) * SPEC_BS + tid] = ((unsigned long long)t << 32) | (unsigned)z;
@@ -417,6 +446,9 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
         rec = srec_pack(y, lab, dmy);
         tmp[nrec++] = rec;
         sig = smix(sig, rec);
+#ifdef MSEG_SPEC_PROF
+        pf_write += (long long)__builtin_amdgcn_s_memtime() - q2;
+#endif
       }
     }  // ex
     if (dg) {
@@ -480,6 +512,15 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
       atomicMax(&ctl->spec.rmax, (unsigned long long)tot);
     }
   }
+#ifdef MSEG_SPEC_PROF
+  if (ws.diag) {  // bank 2 (msg_set_diag 3): cascade pops, queue entries scanned, phase cycles
+    atomicAdd(&ws.diag[16], (unsigned long long)pf_n);
+    atomicAdd(&ws.diag[17], (unsigned long long)pf_q);
+    atomicAdd(&ws.diag[18], (unsigned long long)pf_sel);
+    atomicAdd(&ws.diag[19], (unsigned long long)pf_load);
+    atomicAdd(&ws.diag[20], (unsigned long long)pf_write);
+  }
+#endif
   __syncthreads();
   if (tid == 0) {
     atomicAdd((unsigned long long*)&ctl->spec.execs, (unsigned long long)s_exec);

@@ -1777,34 +1777,42 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
       if (tid == 0) atomicAdd(&arrive[blockIdx.x & 7], 1u);
       return;
     }
-    // rows of the earlier chunks: a quarter per thread group, every load issued before the sums
+    // everything this block reads, issued together (one round trip): the earlier sub-rounds'
+    // descriptors of its chunk, its own items, the old tails, the earlier chunks' histogram rows
+    const int sub = vb % SUBS;
+    unsigned long long dj[SUBS - 1];
+#pragma unroll
+    for (int k = 0; k < SUBS - 1; ++k) dj[k] = (k < sub) ? ws.desc[ch * CH + k * 1024 + tid] : 0ull;
+    const int i = i0 + tid;
+    const bool valid = i < ncommit;
+    unsigned long long dself = 0;
+    int pself = 0, lself = 0;
+    if (valid) {
+      dself = ws.desc[i];
+      pself = ws.ipx[i];
+      lself = (int)(uint32_t)ws.tl[i];
+    }
+    const int qt = (tid < NQ) ? ctl->qtail[tid] : 0;
     gpart[tid >> 8][tid & (NQ - 1)] = rows_sum(ws.cnt, tid >> 8, ch, tid & (NQ - 1));
     if (tid < NQ) {
 #pragma unroll
       for (int k = 0; k < NW; ++k) wcnt[k][tid] = 0;
     }
     __syncthreads();
-    if (tid < NQ) run[tid] = ctl->qtail[tid] + gpart[0][tid] + gpart[1][tid] + gpart[2][tid] + gpart[3][tid];
+    if (tid < NQ) run[tid] = qt + gpart[0][tid] + gpart[1][tid] + gpart[2][tid] + gpart[3][tid];
     __syncthreads();  // this block's reads of the control block and of the rows are complete
     if (tid == 0) atomicAdd(&arrive[blockIdx.x & 7], 1u);
-    for (int j = ch * CH + tid; j < i0; j += 1024) {  // earlier sub-rounds of this chunk
-      const unsigned long long d = ws.desc[j];
-      const unsigned m = (unsigned)(d >> 32) & 15u;
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if ((m >> k) & 1u) atomicAdd(&run[(d >> (8 * k)) & 255], 1);
+    for (int k = 0; k < SUBS - 1; ++k) {  // pushes of the earlier sub-rounds of this chunk
+      const unsigned m = (unsigned)(dj[k] >> 32) & 15u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if ((m >> e) & 1u) atomicAdd(&run[(dj[k] >> (8 * e)) & 255], 1);
     }
-    const int i = i0 + tid;
-    const bool valid = i < ncommit;
-    unsigned mask = 0, lvls = 0;
-    long long p = 0;
-    if (valid) {
-      const unsigned long long d = ws.desc[i];
-      mask = (unsigned)(d >> 32) & 15u;
-      lvls = (unsigned)d;
-      p = ws.ipx[i];
-      st_state(ws, p, (int32_t)(uint32_t)ws.tl[i]);
-    }
+    const unsigned mask = (unsigned)(dself >> 32) & 15u;
+    const unsigned lvls = (unsigned)dself;
+    const long long p = pself;
+    if (valid) st_state(ws, p, lself);
     int pos[4] = {0, 0, 0, 0};
     wave_rank(mask, lvls, pos, wcnt[wv]);
     __syncthreads();
@@ -2342,7 +2350,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     s_specgo = 0;
     s_lazyx = 0;
     s_serx = 0;
-    s_specblk = ws.scl ? ctl->spec.block : -1;  // -1: engine off
+    s_specblk = ws.spx ? ctl->spec.block : -1;  // -1: engine off
     s_specool = ctl->spec.cool;
   }
   if (tid < NQ) {
@@ -2868,7 +2876,7 @@ __global__ __launch_bounds__(64) void k_serial(Ws ws, int iter) {
     }
     if (lane == 0) {
       s_err = 0;
-      s_specblk = ws.scl ? ctl->spec.block : -1;  // -1: engine off
+      s_specblk = ws.spx ? ctl->spec.block : -1;  // -1: engine off
       s_specool = ctl->spec.cool;
     }
     wave_sync();

@@ -80,12 +80,21 @@ constexpr int SPEC_RL = MSEG_SPEC_RL;      // records per execution (lane scratc
 constexpr int SPEC_ROUNDS_MAX = 64; // rounds per generation before the stable prefix is committed
 constexpr int SPEC_FT = 1024;       // items per k_spec_flatten tile
 constexpr int SPEC_QUIET = 4096;    // a generation this large without a cascade ends the regime
-constexpr int SPEC_SERIAL_TICKS = 50;        // ~0.5 us per serial pop (10 ns ticks): a regime
+constexpr int SPEC_SERIAL_TICKS = 100;       // ~1 us per serial pop (10 ns ticks): a regime
 constexpr int SPEC_JUDGE_GENS = 16;          // slower than that per committed pop (its fallbacks'
                                              // serial pops included), after this many
                                              // generations, ends for
 constexpr int SPEC_COOL_POPS = 65536;        // this many serial pops (doubling per repeat)
 constexpr int SPEC_JUDGE_TICKS = 200000;     // slow generations are judged after 4 once 2 ms passed
+
+// A tiled pixel's speculative-generation words (k_spec_round reads a neighbour's whole record
+// with two 16-B loads).
+struct alignas(32) SpecPx {
+  unsigned long long cl[2];  // round claims by round parity: {round tag, inverted rank, popped}
+  unsigned long long fin;    // final claim: {generation tag, popped, label}
+  int lab[2];                // label of the popper, by round parity
+};
+static_assert(sizeof(SpecPx) == 32, "SpecPx is one 32-byte record");
 
 struct SpecCtl {
   unsigned T;     // current round tag: round claims in scl[T & 1], labels in slab[T & 1]
@@ -193,11 +202,10 @@ struct Ws {
   unsigned long long* diag;  // nullptr = off; else 8 counters (msg_set_diag)
   int* hmir;         // host-mapped progress mirror {iteration, done, error, remaining, spec, spec_want,
                      // fast batch, serial pending}
-  // speculative generations (nullptr when the engine is off); claims and labels are indexed by
-  // tiled pixel like mk, one array of snp entries per round parity
-  unsigned long long* scl;   // 2 x snp round claims {tag, rank, popped}
-  unsigned long long* sfin;  // snp final claims {generation tag, popped, label}
-  int32_t* slab;             // 2 x snp labels of popped pixels
+  // speculative generations (nullptr when the engine is off): one 32-byte record per tiled
+  // pixel (indexed like mk) holding both round parities' claims and labels and the final claim,
+  // so that a pixel's view is one 128-B line instead of five arrays
+  SpecPx* spx;
   unsigned long long* stl;   // SPEC_WIN top-pop granules {round tag, label}
   unsigned long long* slog;  // generation log: records {label, dmask, pixel}
   int4* srec;                // 2 x SPEC_WIN {log base, records, round tag, capacity overflow} per round parity

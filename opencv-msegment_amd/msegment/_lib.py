@@ -23,6 +23,7 @@ MSG_ERANGE = -6
 
 MSG_NC_GISTO_DIAP = 0x1
 MSG_NC_MULTI_OTSU = 0x2
+MSG_CREATE_HIGH_PRIORITY = 0x1
 MSG_NC_MEDIAN_BLUR = 0x4
 MSG_NC_BILATERAL = 0x8
 

@@ -9,5 +9,10 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -k "$K" --timeout 240 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -n 5 "$OUT/pytest_gpu.log"
 case $rc in 0|1|5) ;; *) echo "STOP"; exit $rc ;; esac
+if [ -n "${SPEC_PHASES:-}" ]; then
+  MSEGMENT_LIB=$PWD/opencv-msegment_amd/msegment/libmsegment_specprof.so timeout -k 10 300 python scripts/spec_phases.py $SPEC_PHASES > "$OUT/spec_phases.log" 2>&1
+  rc=$?; echo "spec_phases rc=$rc"; cat "$OUT/spec_phases.log" | cut -c1-400
+  case $rc in 0|1) ;; *) echo "STOP"; exit $rc ;; esac
+fi
 timeout -k 10 600 python bench.py "$@" > "$OUT/bench.log" 2>&1
-rc=$?; echo "bench rc=$rc"; tail -n 3 "$OUT/bench.log" | cut -c1-3000
+rc=$?; echo "bench rc=$rc"; python scripts/bench_summary.py "$OUT/bench.log"

@@ -1,0 +1,47 @@
+"""Where a speculative generation's cascade pops spend their time (diagnostic build only:
+libmsegment built with -DMSEG_SPEC_PROF, selected through MSEGMENT_LIB).  Per input: rounds,
+executions per pop, and for the cascade pops inside k_spec_round the lane-summed s_memtime cycles
+of queue selection (the per-lane LDS queue scan + shift), the loads (weights + the four neighbour
+views) and the writes (claims, labels, records), with the average queue length scanned.
+usage: MSEGMENT_LIB=.../libmsegment_specprof.so python scripts/spec_phases.py mosaic_noise_1024_s1 ..."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "opencv-msegment_amd")]
+
+import torch  # noqa: E402
+
+import msegment  # noqa: E402
+from msegment import synth  # noqa: E402
+
+
+def main():
+    seg = msegment.Segmenter(0)
+    dev = torch.device("cuda", 0)
+    for nm in sys.argv[1:]:
+        kind, S, seed = nm.rsplit("_", 2)
+        S = int(S)
+        img, m, _ = synth.frame(kind, S, S, int(seed[1:]))
+        ti, tm = torch.from_numpy(img).to(dev), torch.from_numpy(m).to(dev)
+        tl = torch.empty_like(tm)
+        seg.watershed_dev(ti, tm, tl)
+        torch.cuda.synchronize()
+        seg.set_diag(3)
+        seg.watershed_dev(ti, tm, tl)
+        torch.cuda.synchronize()
+        st = seg.stats()
+        seg.set_diag(False)
+        d = st["diag"]
+        n = max(1, d[0])
+        tot = max(1, d[2] + d[3] + d[4])
+        print("%s: gens %d rounds %d execs/pop %.2f | cascade pops (lane sums) %d, avg queue %.2f | cycles per cascade pop:"
+              " select %.0f (%.0f%%), loads %.0f (%.0f%%), writes %.0f (%.0f%%)" % (
+                  nm, st["spec_generations"], st["spec_rounds"], st["spec_executions"] / max(1, st["pops"]), d[0],
+                  d[1] / n, d[2] / n, 100.0 * d[2] / tot, d[3] / n, 100.0 * d[3] / tot, d[4] / n, 100.0 * d[4] / tot),
+              flush=True)
+    seg.close()
+
+
+if __name__ == "__main__":
+    main()

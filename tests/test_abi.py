@@ -52,5 +52,6 @@ def test_python_constants_match_header():
     defs = dict(re.findall(r"#define (MSG_\w+)\s+\(?(-?(?:0x)?[0-9a-fA-F]+)u?\)?", hdr))
     assert int(defs["MSG_NKERNELS"], 0) == _lib.NKERNELS
     for name in ("MSG_OK", "MSG_EINVAL", "MSG_EHIP", "MSG_ENOMEM", "MSG_ETIMEOUT", "MSG_ESTATE", "MSG_ERANGE",
-                 "MSG_NC_GISTO_DIAP", "MSG_NC_MULTI_OTSU", "MSG_NC_MEDIAN_BLUR", "MSG_NC_BILATERAL"):
+                 "MSG_NC_GISTO_DIAP", "MSG_NC_MULTI_OTSU", "MSG_NC_MEDIAN_BLUR", "MSG_NC_BILATERAL",
+                 "MSG_CREATE_HIGH_PRIORITY"):
         assert int(defs[name], 0) == getattr(_lib, name), name
