@@ -400,8 +400,11 @@ def stress_line(seg, S, sync, dev, steps, cpu=True, kind="mosaic_noise", seed=2)
     st = seg.stats()
     out["flood"] = {"batches": st["batches"], "pops": st["pops"], "items": st["items"],
                     "spec_generations": st["spec_generations"], "spec_rounds": st["spec_rounds"],
-                    "spec_executions": st["spec_executions"], "spec_fallbacks": st["spec_fallbacks"],
-                    "executions_per_pop": round(st["spec_executions"] / max(1, st["pops"]), 3)}
+                    "spec_executions": st["spec_executions"], "spec_replays": st["spec_replays"],
+                    "spec_fallbacks": st["spec_fallbacks"],
+                    "executions_per_pop": round(st["spec_executions"] / max(1, st["pops"]), 3),
+                    # executions that ran their cascade pop by pop (the rest replayed the last round's)
+                    "full_executions_per_pop": round((st["spec_executions"] - st["spec_replays"]) / max(1, st["pops"]), 3)}
     kern = kernel_roofline(prof, st, S * S, 1)
     out["kernels"] = kern
     top = kern[0] if kern else None

@@ -72,6 +72,9 @@ typedef struct msg_stats {
     int64_t spec_executions;    /* item executions over all rounds                              */
     int64_t spec_cascade_pops;  /* committed pops inside cascades (below the generation level)  */
     int64_t spec_fallbacks;     /* overflowing executions handed to serial pops                 */
+    int64_t spec_replays;       /* executions whose cascade was replayed from the previous
+                                   round's log (no input changed): spec_executions - spec_replays
+                                   cascades were run pop by pop                                 */
 } msg_stats;
 
 #define MSG_NKERNELS 24

@@ -57,6 +57,7 @@ struct msg_ctx {
   unsigned long long *d_ssig = nullptr, *d_stmp = nullptr, *d_sflag = nullptr;
   int4* d_srec = nullptr;
   int2* d_sfrec = nullptr;
+  unsigned* d_sdirt = nullptr;
   unsigned stag = 0;            // last round tag used (claims carry it; never reused)
   int spec_grid = 0;            // k_spec_round blocks
   // staging for the host-buffer entry points
@@ -233,13 +234,14 @@ void free_flood(msg_ctx* c) {
 
 void free_spec(msg_ctx* c) {
   dfree(c->d_spx); dfree(c->d_stl); dfree(c->d_slog); dfree(c->d_ssig);
-  dfree(c->d_stmp); dfree(c->d_sflag); dfree(c->d_srec); dfree(c->d_sfrec);
+  dfree(c->d_stmp); dfree(c->d_sflag); dfree(c->d_srec); dfree(c->d_sfrec); dfree(c->d_sdirt);
   c->spec_np = c->spec_logcap = 0;
   c->stag = 0;
 }
 
-// Speculative-generation workspace for np tiled pixels (n frame pixels): round claims and labels
-// (2 x 12 B), final claims (8 B) and the generation log (32 B) per pixel, per-rank arrays for
+// Speculative-generation workspace for np tiled pixels (n frame pixels): the SpecPx record (round
+// claims and labels of both parities, final claim: 32 B), change marks (2 x 4 B) and the
+// generation log (32 B) per pixel, per-rank arrays for
 // SPEC_WIN items, SPEC_RL records of scratch per k_spec_round thread.  Tags start at 1 on a
 // zeroed claim space and are never reused; near 2^31 the space is zeroed again.
 int ensure_spec(msg_ctx* c, long long np, long long n, hipStream_t st) {
@@ -249,6 +251,7 @@ int ensure_spec(msg_ctx* c, long long np, long long n, hipStream_t st) {
     free_spec(c);
     const long long slots = (long long)c->spec_grid * SPEC_BS;
     HIPCHK(c, hipMalloc((void**)&c->d_spx, np * sizeof(SpecPx)));
+    HIPCHK(c, hipMalloc((void**)&c->d_sdirt, 2 * np * sizeof(unsigned)));
     HIPCHK(c, hipMalloc((void**)&c->d_stl, (size_t)SPEC_WIN * 8));
     HIPCHK(c, hipMalloc((void**)&c->d_slog, logcap * 8));
     HIPCHK(c, hipMalloc((void**)&c->d_srec, (size_t)2 * SPEC_WIN * sizeof(int4)));
@@ -260,6 +263,7 @@ int ensure_spec(msg_ctx* c, long long np, long long n, hipStream_t st) {
     c->spec_logcap = logcap;
   }
   HIPCHK(c, hipMemsetAsync(c->d_spx, 0, c->spec_np * sizeof(SpecPx), st));
+  HIPCHK(c, hipMemsetAsync(c->d_sdirt, 0, 2 * c->spec_np * sizeof(unsigned), st));
   HIPCHK(c, hipMemsetAsync(c->d_stl, 0, (size_t)SPEC_WIN * 8, st));
   HIPCHK(c, hipMemsetAsync(c->d_sflag, 0, (size_t)(SPEC_WIN / SPEC_FT + 2) * 8, st));
   c->stag = 0;
@@ -418,6 +422,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
     ws.slog = on ? c->d_slog : nullptr; ws.srec = on ? c->d_srec : nullptr;
     ws.ssig = on ? c->d_ssig : nullptr; ws.sfrec = on ? c->d_sfrec : nullptr;
     ws.stmp = on ? c->d_stmp : nullptr; ws.sflag = on ? c->d_sflag : nullptr;
+    ws.sdirt = on ? c->d_sdirt : nullptr;
     ws.snp = on ? c->spec_np : 0;
     ws.slogcap = on ? c->spec_logcap : 0;
     ws.spec_lazy = (spec && !on) ? 1 : 0;
@@ -549,6 +554,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   c->stats.spec_generations = tail.spec.gens;
   c->stats.spec_rounds = tail.spec.rounds_total;
   c->stats.spec_executions = tail.spec.execs;
+  c->stats.spec_replays = tail.spec.replays;
   c->stats.spec_cascade_pops = tail.spec.cpops;
   c->stats.spec_fallbacks = tail.spec.fallbacks;
   if (spec_bound) c->stag = tail.spec.T;

@@ -116,15 +116,47 @@ __device__ __forceinline__ int spec_decide(const SpecView& V, const SpecRec& r, 
   return (r.s >= WSHED) ? r.s : INQ;
 }
 
-// top-pop granule of item k as item j may use it in round T: this round's, or a final item's
-__device__ __forceinline__ bool spec_granule(const Ws& ws, int k, int P, unsigned T, unsigned G, int& v) {
+// top-pop granule of item k as item j may use it in round T: this round's, or a final item's.
+// Word: label | round tag << 32 | (label differs from item k's previous round) << 63; chg
+// collects that bit of the non-final items read (an input of the reader changed).
+constexpr unsigned long long SPEC_GDIFF = 1ull << 63;
+__device__ __forceinline__ bool spec_granule(const Ws& ws, int k, int P, unsigned T, unsigned G, int& v, bool& chg) {
   const unsigned long long g = ld_ag64(ws.stl + k);
-  const unsigned tg = (unsigned)(g >> 32);
+  const unsigned tg = (unsigned)(g >> 32) & 0x7fffffffu;
   if (tg == T || (k < P && tg >= G && tg <= T)) {
     v = (int)(uint32_t)g;
+    if (k >= P && (g & SPEC_GDIFF)) chg = true;
     return true;
   }
   return false;
+}
+
+// Replay (round T >= G + 2): item j's top pop came out as in round T - 1 (same record, no changed
+// granule read) and no pixel its previous cascade viewed -- the neighbours of its pops -- was
+// marked in round T - 1 (a claim of a changed execution, old or new): its inputs are those of
+// round T - 1, so its cascade is that round's, replayed from the log without the dependent
+// round trip per pop.  Checks first (all loads independent), then the claims.
+__device__ __forceinline__ bool spec_replay_clean(const Ws& ws, int base, int nrec, int ppar, unsigned T,
+                                                  const int* nbp) {
+  const unsigned* const dirt = ws.sdirt + (size_t)ppar * ws.snp;
+  const unsigned tp = T - 1u;
+  bool dirty = false;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dirty |= dirt[nbp[d]] == tp;
+  const int Wt = ws.Wt, marg = ws.marg;
+  for (int k0 = 1; k0 < nrec && !dirty; k0 += 4) {
+    unsigned long long r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = (k0 + k < nrec) ? ws.slog[base + k0 + k] : 0ull;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k0 + k >= nrec) continue;
+      const int yb = (int)(r[k] & 0x0fffffffu) + marg;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) dirty |= dirt[nbi(yb, d, Wt) - marg] == tp;
+    }
+  }
+  return !dirty;
 }
 
 // End of a round (last block): grow the stable prefix, or hand the generation to the commit.
@@ -135,10 +167,12 @@ __device__ void spec_finalize(Ctl* ctl, int P, int n, unsigned T, unsigned G, un
     s.rmax = 0;
   }
   // written by this kernel's atomics: read at L2, not through a line cached at kernel start
-  const int fc = __hip_atomic_load(&s.fc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int ov = __hip_atomic_load(&s.ovfr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int fc = __hip_atomic_load(&ctl->sfc.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int ov = __hip_atomic_load(&ctl->sovf.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int newP = min(fc, n);
   s.rounds_total += 1;
+  s.ov2 = s.ov1;
+  s.ov1 = ov;
   if (newP >= n) {
     s.Pprom = P;
     s.P = n;
@@ -158,9 +192,9 @@ __device__ void spec_finalize(Ctl* ctl, int P, int n, unsigned T, unsigned G, un
     s.P = newP;
     s.T = T + 1;
     s.rounds += 1;
-    s.deal = P;
-    s.fc = NONE;
-    s.ovfr = NONE;
+    ctl->sdeal.v = P;
+    ctl->sfc.v = NONE;
+    ctl->sovf.v = NONE;
   }
   s.ticket = 0;
 }
@@ -171,12 +205,16 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
   Ctl* ctl = ws.ctl;
   if (ctl->bat.mode != 3 || ctl->spec.state != 1 || ctl->error) return;
   __shared__ unsigned long long lq[SPEC_QCAP * SPEC_BS];  // per-lane cascade queues, [entry][lane]
-  __shared__ int s_exec;
+  __shared__ int s_exec, s_rep;
   const int tid = threadIdx.x, lane = lane_id();
-  if (tid == 0) s_exec = 0;
+  if (tid == 0) s_exec = s_rep = 0;
   const unsigned T = ctl->spec.T, G = ctl->spec.G;
   const int P = ctl->spec.P, n = ctl->spec.n, L = ctl->spec.L, bstart = ctl->spec.bstart;
   const int par = (int)(T & 1u), ppar = (int)((T - 1u) & 1u);
+  // replays need complete change marks: no overflowing execution (claims never logged in full)
+  // below the item in the last two rounds
+  const int ovlim = min(ctl->spec.ov1, ctl->spec.ov2);
+  int nrep = 0;
   SpecView V;
   V.spx = ws.spx;
   V.par = par;
@@ -198,7 +236,9 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
   __syncthreads();
   while (!stop) {
     int r0 = 0;
-    if (lane == 0) r0 = atomicAdd(&ctl->spec.deal, 64);
+    // (pre-checking the word with a load before the atomic, sharding the log counter per
+    // blockIdx % 8 and skipping rank-minimum atomics already beaten measured 26% slower)
+    if (lane == 0) r0 = atomicAdd(&ctl->sdeal.v, 64);
     r0 = __shfl(r0, 0);
     if (r0 >= n) break;
     const int j = r0 + lane;
@@ -225,7 +265,9 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) dep[k] = -1;
     int base_lab = 0;
+    unsigned long long gold = 0;
     if (ex) {
+      gold = ld_ag64(ws.stl + j);
       p = ws.qbuf[bstart + j];
       wp = (unsigned)ws.w4[p];
       const int pb = p + marg;
@@ -270,6 +312,7 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
     int mylab = 0;
     unsigned pm = 0;
     bool ovf = false, cap = false;  // unstable; capacity overflow
+    bool gchg = T < G + 2u;         // a granule input changed since round T - 1 (or unknown)
     long long t0 = 0;
     int spins = 0;
     for (;;) {
@@ -280,7 +323,7 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
         for (int d = 0; d < 4; ++d) {
           if (dep[d] < 0) continue;
           int v;
-          if (spec_granule(ws, dep[d], P, T, G, v)) {
+          if (spec_granule(ws, dep[d], P, T, G, v, gchg)) {
             if (v > 0) lab = fold_lab(lab, v);
           } else {
             unk = true;
@@ -293,7 +336,9 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
           }
           mylab = lab;
           labd = true;
-          st_ag64(ws.stl + j, etag | (uint32_t)lab);
+          if (unk) gchg = true;
+          const bool same = T > G && (unsigned)(gold >> 32 & 0x7fffffffu) == T - 1u && (int)(uint32_t)gold == lab;
+          st_ag64(ws.stl + j, etag | (uint32_t)lab | (same ? 0ull : SPEC_GDIFF));
         }
       }
       if (labd && !pushd) {
@@ -311,7 +356,7 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
               const int r = dep[4 + 3 * d + k];
               if (r < 0) continue;
               int v;
-              if (spec_granule(ws, r, P, T, G, v)) {
+              if (spec_granule(ws, r, P, T, G, v, gchg)) {
                 if (v > 0) lose = true;  // that item pushed the neighbour first
               } else {
                 u = true;
@@ -320,6 +365,8 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
             if (!lose) {
               if (u) und = true;
               else m |= 1u << d;
+            } else if (u) {
+              gchg = true;
             }
           }
           if (!und) {
@@ -349,21 +396,24 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
     const long long tkb = dg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long sig = 0;
     int nrec = 0;
+    int rbase = -1;  // >= 0: the cascade was replayed from the previous round's log records here
     if (ex) {
-      // ---- the top pop's writes, then the cascade (levels < L, lowest first, FIFO) ----
-      claim_max(&spx[p].cl[par], spec_claim(T, j, 1u));
-      st_ag32(&spx[p].lab[par], mylab);
+      // ---- the top pop, then the cascade (levels < L, lowest first, FIFO) ----
+      // Every pop's writes (claims, label, record) are issued AFTER the loads of the next pop's
+      // neighbours: the wave's memory counter retires in issue order, so a load issued behind
+      // stores waits for their acknowledgements too.  The next pop therefore sees its
+      // predecessor's writes through a patch (that pop's pixel and pushes) instead of memory;
+      // everything older was issued before its loads.
       int nq = 0;
-      unsigned dm = 0;
+      unsigned dm = 0, ppm = 0;  // deferred pushes; the pending pop's pushes (all levels)
       if (mylab != WSHED) {
   #pragma unroll
         for (int d = 0; d < 4; ++d) {
           if (!((pm >> d) & 1u)) continue;
-          const int z = nbp[d];
-          claim_max(&spx[z].cl[par], spec_claim(T, j, 0u));
+          ppm |= 1u << d;
           const unsigned t = (wp >> (8 * d)) & 255u;
           if ((int)t < L) {
-            if (nq < SPEC_QCAP) lq[(nq++) * SPEC_BS + tid] = ((unsigned long long)t << 32) | (unsigned)z;
+            if (nq < SPEC_QCAP) lq[(nq++) * SPEC_BS + tid] = ((unsigned long long)t << 32) | (unsigned)nbp[d];
             else ovf = cap = true;
           } else {
             dm |= 1u << d;
@@ -372,18 +422,43 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
       }
       unsigned long long rec = srec_pack(p, mylab, dm);
       sig = smix(0x6a09e667f3bcc908ull, rec);
-      tmp[0] = rec;
       nrec = 1;
-      while (nq > 0 && !ovf) {
-        if (nrec >= SPEC_RL) {
-          ovf = cap = true;
-          break;
+      // the pending pop: its writes are not issued yet
+      int py = p, plab = mylab;
+      int pz[4] = {nbp[0], nbp[1], nbp[2], nbp[3]};
+      auto issue_writes = [&](int k) {  // pop k of this execution: pixel py, label plab, pushes ppm
+        claim_max(&spx[py].cl[par], spec_claim(T, j, 1u));
+        st_ag32(&spx[py].lab[par], plab);
+  #pragma unroll
+        for (int d = 0; d < 4; ++d)
+          if ((ppm >> d) & 1u) claim_max(&spx[pz[d]].cl[par], spec_claim(T, j, 0u));
+        tmp[k] = rec;
+      };
+      if (nq > 0 && !ovf && !gchg && j < ovlim) {
+        const int4 pr = ws.srec[(size_t)ppar * SPEC_WIN + j];
+        if (pr.z == (int)(T - 1u) && pr.y > 1 && ws.slog[pr.x] == rec &&
+            spec_replay_clean(ws, pr.x, pr.y, ppar, T, nbp)) {
+          issue_writes(0);
+          for (int k = 1; k < pr.y; ++k) {  // round T's claims, as the cascade writes them
+            const unsigned long long r = ws.slog[pr.x + k];
+            const int y = (int)(r & 0x0fffffffu);
+            const unsigned dmy = (unsigned)(r >> 28) & 15u;
+            claim_max(&spx[y].cl[par], spec_claim(T, j, 1u));
+            st_ag32(&spx[y].lab[par], (int)(uint32_t)(r >> 32));
+  #pragma unroll
+            for (int d = 0; d < 4; ++d)
+              if ((dmy >> d) & 1u) claim_max(&spx[nbi(y + marg, d, Wt) - marg].cl[par], spec_claim(T, j, 0u));
+            sig = smix(sig, r);
+          }
+          nrec = pr.y;
+          rbase = pr.x;
+          nq = 0;
+          ppm = 0;
+          py = -1;
         }
-#ifdef MSEG_SPEC_PROF
-        const long long q0 = (long long)__builtin_amdgcn_s_memtime();
-        pf_n += 1;
-        pf_q += nq;
-#endif
+      }
+      // next pop: the oldest entry of the lowest level in the lane's LDS queue
+      auto select = [&]() -> int {
         int bi = 0;
         unsigned long long be = lq[tid];
         for (int k = 1; k < nq; ++k) {
@@ -395,23 +470,49 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
         }
         for (int k = bi; k + 1 < nq; ++k) lq[k * SPEC_BS + tid] = lq[(k + 1) * SPEC_BS + tid];
         --nq;
-        const int y = (int)(uint32_t)be;
-#ifdef MSEG_SPEC_PROF
-        const long long q1 = (long long)__builtin_amdgcn_s_memtime();
-        pf_sel += q1 - q0;
-#endif
-        const unsigned wy = (unsigned)ws.w4[y];
+        return (int)(uint32_t)be;
+      };
+      int y = 0;
+      unsigned wy = 0;
+      SpecRec r0, r1, r2, r3;  // four named records (an indexed array of them lands in scratch)
+      int nby[4];
+      auto issue_loads = [&]() {
+        wy = (unsigned)ws.w4[y];
         const int yb = y + marg;
-        int nby[4], v[4];
   #pragma unroll
         for (int d = 0; d < 4; ++d) nby[d] = nbi(yb, d, Wt) - marg;
-        {  // four named records (an indexed array of them lands in scratch)
-          const SpecRec r0 = spec_load(ws, V, nby[0]), r1 = spec_load(ws, V, nby[1]);
-          const SpecRec r2 = spec_load(ws, V, nby[2]), r3 = spec_load(ws, V, nby[3]);
-          v[0] = spec_decide(V, r0, j, true);
-          v[1] = spec_decide(V, r1, j, true);
-          v[2] = spec_decide(V, r2, j, true);
-          v[3] = spec_decide(V, r3, j, true);
+        r0 = spec_load(ws, V, nby[0]);
+        r1 = spec_load(ws, V, nby[1]);
+        r2 = spec_load(ws, V, nby[2]);
+        r3 = spec_load(ws, V, nby[3]);
+      };
+      bool more = nq > 0 && !ovf;
+      if (more) {
+        y = select();
+        issue_loads();
+      }
+      if (py >= 0) issue_writes(0);
+      while (more) {
+        if (nrec >= SPEC_RL) {
+          ovf = cap = true;
+          break;
+        }
+#ifdef MSEG_SPEC_PROF
+        const long long q1 = (long long)__builtin_amdgcn_s_memtime();
+        pf_n += 1;
+        pf_q += nq + 1;
+#endif
+        int v[4];
+        v[0] = spec_decide(V, r0, j, true);
+        v[1] = spec_decide(V, r1, j, true);
+        v[2] = spec_decide(V, r2, j, true);
+        v[3] = spec_decide(V, r3, j, true);
+  #pragma unroll
+        for (int d = 0; d < 4; ++d) {  // the pending pop's writes, not in memory yet
+          if (nby[d] == py) v[d] = plab;
+  #pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (((ppm >> e) & 1u) && nby[d] == pz[e]) v[d] = INQ;
         }
         int lab = 0;
   #pragma unroll
@@ -425,29 +526,44 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
           ovf = true;
           lab = WSHED;
         }
-        claim_max(&spx[y].cl[par], spec_claim(T, j, 1u));
-        st_ag32(&spx[y].lab[par], lab);
-        unsigned dmy = 0;
+        unsigned dmy = 0, pmy = 0;
         if (lab != WSHED) {
   #pragma unroll
           for (int d = 0; d < 4; ++d) {
             if (v[d] != 0) continue;
-            const int z = nby[d];
-            claim_max(&spx[z].cl[par], spec_claim(T, j, 0u));
+            pmy |= 1u << d;
             const unsigned t = (wy >> (8 * d)) & 255u;
             if ((int)t < L) {
-              if (nq < SPEC_QCAP) lq[(nq++) * SPEC_BS + tid] = ((unsigned long long)t << 32) | (unsigned)z;
-            else ovf = cap = true;
+              if (nq < SPEC_QCAP) lq[(nq++) * SPEC_BS + tid] = ((unsigned long long)t << 32) | (unsigned)nby[d];
+              else ovf = cap = true;
             } else {
               dmy |= 1u << d;
             }
           }
         }
         rec = srec_pack(y, lab, dmy);
-        tmp[nrec++] = rec;
         sig = smix(sig, rec);
+        py = y;
+        plab = lab;
+        ppm = pmy;
+  #pragma unroll
+        for (int d = 0; d < 4; ++d) pz[d] = nby[d];
+        const int k = nrec++;
+        more = nq > 0 && !ovf;
 #ifdef MSEG_SPEC_PROF
-        pf_write += (long long)__builtin_amdgcn_s_memtime() - q2;
+        const long long q3 = (long long)__builtin_amdgcn_s_memtime();
+#endif
+        if (more) {
+          y = select();
+          issue_loads();
+        }
+#ifdef MSEG_SPEC_PROF
+        const long long q4 = (long long)__builtin_amdgcn_s_memtime();
+        pf_sel += q4 - q3;
+#endif
+        issue_writes(k);
+#ifdef MSEG_SPEC_PROF
+        pf_write += (long long)__builtin_amdgcn_s_memtime() - q4 + (q3 - q2);
 #endif
       }
     }  // ex
@@ -457,7 +573,7 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
       maxrec = max(maxrec, nrec);
     }
     // ---- log space for the wave's records (one atomic per wave), signatures, change words ----
-    const int want = (ex && !ovf) ? nrec : 0;
+    const int want = (ex && !ovf && rbase < 0) ? nrec : 0;
     int incl = want;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -466,12 +582,12 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
     }
     const int wtot = __shfl(incl, 63);
     int wbase = 0;
-    if (lane == 0 && wtot) wbase = atomicAdd(&ctl->spec.logtop, wtot);
+    if (lane == 0 && wtot) wbase = atomicAdd(&ctl->slogtop.v, wtot);
     wbase = __shfl(wbase, 0);
     int fcand = NONE, ocand = NONE;
     if (ex) {
-      const int base = wbase + incl - want;
-      if (!ovf) {
+      const int base = rbase >= 0 ? rbase : wbase + incl - want;
+      if (!ovf && rbase < 0) {
         if ((long long)base + nrec > ws.slogcap) ovf = cap = true;  // generation log full
         else
           for (int k = 0; k < nrec; ++k) ws.slog[base + k] = tmp[k];
@@ -484,6 +600,23 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
                            ws.ssig[(size_t)ppar * SPEC_WIN + j] != sig;
       if (changed) fcand = j;
       if (ovf) ocand = j;
+      if (rbase >= 0) ++nrep;
+      if (changed) {  // mark both executions' claims: round T + 1 replays nothing that viewed them
+        unsigned* const dn = ws.sdirt + (size_t)par * ws.snp;
+        auto mark = [&](unsigned long long r) {
+          const int y = (int)(r & 0x0fffffffu);
+          const unsigned dmy = (unsigned)(r >> 28) & 15u;
+          dn[y] = T;
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+            if ((dmy >> d) & 1u) dn[nbi(y + marg, d, Wt) - marg] = T;
+        };
+        if (rbase < 0)
+          for (int k = 0; k < nrec; ++k) mark(tmp[k]);
+        const int4 pr = ws.srec[(size_t)ppar * SPEC_WIN + j];
+        if (V.hasprev && pr.z == (int)(T - 1u))
+          for (int k = 0; k < pr.y; ++k) mark(ws.slog[pr.x + k]);
+      }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -491,8 +624,9 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
       ocand = min(ocand, __shfl_xor(ocand, o));
     }
     if (lane == 0) {
-      if (fcand != NONE) atomicMin(&ctl->spec.fc, fcand);
-      if (ocand != NONE) atomicMin(&ctl->spec.ovfr, ocand);
+      // ranks are dealt in increasing order: once a lower rank is in, later waves skip the atomic
+      if (fcand != NONE) atomicMin(&ctl->sfc.v, fcand);
+      if (ocand != NONE) atomicMin(&ctl->sovf.v, ocand);
       const int nex = max(0, min(n, r0 + 64) - max(P, r0));
       if (nex) atomicAdd(&s_exec, nex);
     }
@@ -521,9 +655,11 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
     atomicAdd(&ws.diag[20], (unsigned long long)pf_write);
   }
 #endif
+  if (nrep) atomicAdd(&s_rep, nrep);
   __syncthreads();
   if (tid == 0) {
     atomicAdd((unsigned long long*)&ctl->spec.execs, (unsigned long long)s_exec);
+    if (s_rep) atomicAdd((unsigned long long*)&ctl->spec.replays, (unsigned long long)s_rep);
     __threadfence();
     if (atomicAdd(&ctl->spec.ticket, 1) == (int)gridDim.x - 1) {
       __threadfence();

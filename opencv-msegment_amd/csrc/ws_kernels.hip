@@ -790,11 +790,11 @@ __device__ void spec_begin(Ctl* ctl, Batch& nb, int L, int bstart, int navail) {
   s.Pprom = 0;
   s.rounds = 1;
   s.state = 1;
-  s.fc = NONE;
-  s.ovfr = NONE;
-  s.deal = 0;
+  ctl->sfc.v = NONE;
+  ctl->sovf.v = NONE;
+  ctl->sdeal.v = 0;
   s.ticket = 0;
-  s.logtop = 0;
+  ctl->slogtop.v = 0;
   s.fallback = 0;
   s.ftile = 0;
 }

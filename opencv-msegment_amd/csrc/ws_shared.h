@@ -107,11 +107,7 @@ struct SpecCtl {
   int state;      // 0 none, 1 rounds running, 2 ready to flatten
   int on;         // regime: batches are speculative generations
   int block;      // after a fallback: the regime may resume once the lowest level is >= block
-  int fc;         // lowest rank whose execution changed this round (atomicMin)
-  int ovfr;       // lowest rank that overflowed this round (atomicMin)
-  int deal;       // dispatch-order rank dealing
   int ticket;     // blocks finished this round
-  int logtop;     // generation log records used
   int fallback;   // the commit ends the regime (overflow at the stable prefix)
   int ftile;      // k_spec_flatten tile dealing
   int cool;       // serial pops to go before the regime may start again
@@ -121,6 +117,8 @@ struct SpecCtl {
   long long tstart, pstart;  // regime start: s_memrealtime, Ctl.pops
   long long gens, rounds_total, execs, cpops, fallbacks;
   unsigned long long rmax;  // diagnostics: longest wave of this round (10 ns ticks)
+  int ov1, ov2;             // lowest overflowing rank of the last / the one-before-last round
+  long long replays;        // executions whose cascade was replayed from the previous round
 };
 
 // desc word of a batch item: bits 0-31 the 4 edge weights, 32-35 push (or 0-neighbour) mask,
@@ -178,6 +176,15 @@ struct Ctl {
   unsigned hold;     // epoch of a decided batch k_commit_fast declined (k_resolve must not re-run it)
   int pad3;
   unsigned farrive[8];  // k_commit_fast: sub-round blocks done reading, by blockIdx % 8 (zeroed after)
+  // k_spec_round's contended words, one 128-B line each: device-scope atomics on one line
+  // serialise (~11 ns each), and a round issues thousands of them
+  struct alignas(128) Hot {
+    int v;
+    int pad[31];
+  };
+  Hot sdeal;     // dispatch-order rank dealing
+  Hot sfc, sovf; // lowest changed / overflowing rank of this round
+  Hot slogtop;   // generation log records used
 };
 
 static_assert(__builtin_offsetof(Ctl, error) % 8 == 0 && __builtin_offsetof(Ctl, rgive) == __builtin_offsetof(Ctl, error) + 4,
@@ -213,6 +220,8 @@ struct Ws {
   int2* sfrec;               // SPEC_WIN {log base, records} of promoted items
   unsigned long long* stmp;  // lane scratch: SPEC_RL records per k_spec_round thread
   unsigned long long* sflag; // k_spec_flatten tile prefixes {generation tag, inclusive sum}
+  unsigned* sdirt;           // 2 x snp change marks per round parity: round tag of the last changed
+                             // execution whose claims (old or new) covered the pixel
   long long snp;
   long long slogcap;
   int spec_lazy;     // 1: engine enabled, workspace not allocated yet (k_scan reports spec_want)

@@ -187,6 +187,7 @@ int main(int argc, char** argv) {
     }
   }
   unsigned rng = 777;
+  const int genlog = getenv("SPEC_GENLOG") != NULL;
   T = 0;
   for (;;) {
     L = 0;
@@ -196,6 +197,7 @@ int main(int argc, char** argv) {
     if (n > WIN) n = WIN;
     st_gens++;
     G = ++T;
+    const long long gexec0 = st_exec;
     for (int i = 0; i < n; i++) { tpix[i] = q[L].v[q[L].h + i]; rank_of[tpix[i]] = i; rank_tag[tpix[i]] = G; }
     P = 0;
     int rounds = 0, pstart = 0;
@@ -236,6 +238,7 @@ int main(int argc, char** argv) {
     }
     st_rounds += rounds;
     if (rounds > st_maxr) st_maxr = rounds;
+    if (genlog) fprintf(stderr, "gen L=%d n=%d rounds=%d P=%d execs=%lld\n", L, n, rounds, P, st_exec - gexec0);
     int serial_item = (P < n && ex[lastpar[P] = T & 1][P].ovf == 1);  // overflow: the item runs serially after the commit
     // commit items 0..P-1: serial order = rank order, then each item's records in order
     for (int i = 0; i < P; i++) {

@@ -35,11 +35,30 @@ def main():
         d = st["diag"]
         n = max(1, d[0])
         tot = max(1, d[2] + d[3] + d[4])
-        print("%s: gens %d rounds %d execs/pop %.2f | cascade pops (lane sums) %d, avg queue %.2f | cycles per cascade pop:"
+        print("%s: gens %d rounds %d execs/pop %.2f (replayed %.2f) | cascade pops (lane sums) %d, avg queue %.2f | cycles per cascade pop:"
               " select %.0f (%.0f%%), loads %.0f (%.0f%%), writes %.0f (%.0f%%)" % (
-                  nm, st["spec_generations"], st["spec_rounds"], st["spec_executions"] / max(1, st["pops"]), d[0],
+                  nm, st["spec_generations"], st["spec_rounds"], st["spec_executions"] / max(1, st["pops"]),
+                  st["spec_replays"] / max(1, st["pops"]), d[0],
                   d[1] / n, d[2] / n, 100.0 * d[2] / tot, d[3] / n, 100.0 * d[3] / tot, d[4] / n, 100.0 * d[4] / tot),
               flush=True)
+        # wall-clock split of the round kernels (diag bank 1, 10 ns ticks): wave time in top-pop
+        # waits / cascades / whole kernel, and the sum over rounds of each round's longest wave
+        seg.set_diag(1)
+        torch.cuda.synchronize()
+        t0 = torch.cuda.Event(enable_timing=True)
+        t1 = torch.cuda.Event(enable_timing=True)
+        t0.record()
+        seg.watershed_dev(ti, tm, tl)
+        t1.record()
+        torch.cuda.synchronize()
+        st = seg.stats()
+        seg.set_diag(False)
+        d = st["diag"]
+        w = max(1, d[7])
+        print("%s: flood %.1f ms (diag on) | waves %d, per wave: waits %.1f us, cascades %.1f us, kernel %.1f us |"
+              " sum of longest waves %.1f ms over %d rounds (%.1f us/round) | longest cascade %.1f us, most records %d" % (
+                  nm, t0.elapsed_time(t1), d[7], d[0] / w / 100, d[1] / w / 100, d[2] / w / 100, d[5] / 1e5,
+                  st["spec_rounds"], d[5] / 100 / max(1, st["spec_rounds"]), d[6] / 100, d[4]), flush=True)
     seg.close()
 
 

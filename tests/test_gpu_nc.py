@@ -135,6 +135,21 @@ def test_marker_stage_bilateral(seg, d, kind, shape):
     assert np.array_equal(m.cpu().numpy(), mk)
 
 
+def test_bilateral_non_square_partial_blocks(seg):
+    """A 777 x 1000 frame (width not a multiple of 64: partial blocks; rows and columns reflect at
+    both ends) through d = 9 bit-exact -- the large-frame check of the test below on a frame that
+    is neither square nor block-aligned."""
+    torch = _torch()
+    img = synth.mosaic_image(777, 1000, 4, noise=3)
+    g, h, lv, mk = O.marker_stage(img, 4, bilateral_d=9)
+    m = torch.empty((777, 1000), dtype=torch.int32, device="cuda:0")
+    gray = torch.empty((777, 1000), dtype=torch.uint8, device="cuda:0")
+    assert seg.nc_marker_stage_dev(_dev(img), 4, m, _lib.MSG_NC_BILATERAL | _lib.MSG_NC_MASK(9), gray=gray) == lv
+    torch.cuda.synchronize()
+    assert np.array_equal(gray.cpu().numpy(), g)
+    assert np.array_equal(m.cpu().numpy(), mk)
+
+
 def test_bilateral_1024_and_median_precedence(seg):
     """A 1024^2 noisy mosaic through the BILATERIAL branch (d = 9: a 69-tap disc) bit-exact, and
     MEDIAN_BLUR winning when both flags are set (the reference's if / else-if)."""
