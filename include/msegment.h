@@ -118,9 +118,10 @@ int  msg_set_speculative(msg_ctx* ctx, int enable);
  * the three-launch iterations (A/B runs and tests).  Results are identical either way. */
 int  msg_set_fast_commit(msg_ctx* ctx, int enable);
 /* The serial-pop regime (interrupt-dense floods: real photographs, scattered seeds) in a kernel of
- * its own with the flood state cached in LDS (k_serial) instead of inside the one-workgroup batch
- * loop.  Off by default: measured no faster per pop yet.  Results are
- * identical either way. */
+ * its own (k_serial: one wave, queue bookkeeping in registers and LDS records, stores deferred
+ * behind the next pop's loads) instead of inside the one-workgroup batch loop.  Off by default:
+ * ~1.03 us per pop against the in-loop pops' slightly faster flood times (DESIGN.md section 7,
+ * scripts/serial_phases.py for its per-pop split).  Results are identical either way. */
 int  msg_set_serial_kernel(msg_ctx* ctx, int enable);
 
 /* ---- host-buffer entry points (synchronous; strides in BYTES) ---------------------------- */

@@ -49,7 +49,7 @@ struct msg_ctx {
   long long qcap = 0;
   // speculative generations (spec_kernels.hip): allocated on the first flood that may use them
   bool fast = true;             // msg_set_fast_commit: two-launch iterations for large batches
-  bool serk = false;            // msg_set_serial_kernel: serial pops in k_serial (LDS-cached state)
+  bool serk = false;            // msg_set_serial_kernel: serial pops in k_serial (one wave, register queue state)
   bool spec = true;             // msg_set_speculative
   long long spec_np = 0, spec_logcap = 0;
   SpecPx* d_spx = nullptr;       // per tiled pixel: both parities' claims and labels, final claim
@@ -481,7 +481,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
     // does not wait for the host to see it
     ser_seen = ser_seen || (c->serk && c->h_mir[7] != 0);
     for (int g = 0; g < c->group; ++g, ++it) {
-      if (ser_it) {  // serial pops pending: one wave with the LDS-cached state
+      if (ser_it) {  // serial pops pending: k_serial, one wave
         LAUNCH(c, KID_SERIAL, st, k_serial, dim3(1), dim3(64), 0, ws, it);
         continue;
       }

@@ -2621,286 +2621,247 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
 // the host when the progress mirror reports a batch in mode 4 ("serial pops pending", set by
 // k_scan's small-batch loop where it used to pop serially itself).  The same scalar program as
 // serial_loop -- pop the oldest item of the lowest non-empty bucket, fold its labelled
-// neighbours, push its unknown ones in L,R,T,B order -- but the flood state it touches lives in
-// an LDS cache: 2-way set-associative lines of 32 tiled entries (a tile pair, 8 x 4 pixels),
-// states and weights, written back on eviction and at exit (only the entries the loop wrote: a
-// dirty mask per line).  Nothing else touches the flood state while it runs (one kernel at a time
-// on the flood's stream), so the cache needs no coherence.  A pop reads its own line and at most
-// one horizontal and one vertical neighbour line; when all three fall into one set, the third is
-// read and written in global memory directly.  Queue slots stay in global memory (written
-// through; the popped bucket's next 64 slots are prefetched as in serial_loop).  The whole wave
-// runs one uniform program (uniform LDS addresses broadcast); only line fills and write-backs use
-// the lanes separately.
-constexpr int SER_WAYS = 4, SER_SETS = 128, SER_LINES = SER_WAYS * SER_SETS;
-constexpr int SER_RING = 16;  // per-bucket LDS ring of the pixels this launch pushed (queue slots)
-struct SerCache {
-  int st[SER_LINES][32];
-  unsigned w4[SER_LINES][32];
-  int tag[SER_LINES];       // line id (margin-relative tiled index >> 5), -1 empty; set s = ways 4s..4s+3
-  unsigned dirty[SER_LINES];
-  int rr[SER_SETS];         // next way to evict (round robin, skipping the pop's pinned lines)
-};
+// neighbours, push its unknown ones in L,R,T,B order -- laid out for a lone wave's latencies:
+//   * bucket b's {head, tail, base, tail at entry} is one 16-B LDS record (one ds_read_b128), the
+//     non-empty buckets a 256-bit mask in scalar registers (the lowest non-empty bucket is a
+//     find-first-set), the popped bucket's next 64 queue slots one VGPR, and the pixels this
+//     launch pushed a 16-entry LDS ring per bucket (an interrupt cascade pops what it just pushed);
+//   * a pop's one dependent memory round trip is the load of its four neighbours' states and its
+//     weights.  vmcnt counts loads and stores in issue order, so a load issued after a store waits
+//     for that store's acknowledgement too: the previous pop's stores (its label, its pushes'
+//     states and queue slots) are therefore issued AFTER this pop's loads, and the values this
+//     pop loaded from addresses the previous pop wrote are patched in registers.  Every lane
+//     stores the same value to the same address (one request), so the wave's later loads see it.
+constexpr int SER_RING = 16;
 
-__device__ __forceinline__ int ser_set(int L) { return (int)(((unsigned)L * 2654435761u) >> 25); }
+struct SerStat {
+  long long pops = 0, pushes = 0;
+  unsigned long long tsel = 0, tld = 0, tpush = 0;  // MSEG_SER_PROF: s_memtime cycles per phase
+};
+// the previous pop's writes, not yet issued: the label of pixel pp, and its pushes by direction
+// d in mask m (pixel z[d] queued at slot qs[d], state word sv[d]); indexed by the unrolled
+// direction only, so the arrays stay in registers
+struct SerPend {
+  int pp = -1, lab = 0;
+  unsigned m = 0;
+  int z[4], qs[4], sv[4];
+};
 // every value the whole wave computes alike is moved to a scalar register, so the pop's control
 // flow is scalar (no exec-mask bookkeeping around uniform branches)
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-
-// Line L resident in the cache, never evicting lines pa / pb (4 ways: a pop pins at most 3):
-// its slot.  The fill's load is issued before the victim's write-back, so the load's wait
-// (vmcnt, in issue order) does not cover those stores.
-__device__ __forceinline__ int ser_line(SerCache& C, int* mkb, const unsigned* w4b, int L, int pa, int pb,
-                                        long long& fills) {
-  const int set = ser_set(L), s0 = SER_WAYS * set;
-  const int t0 = uni(C.tag[s0]), t1 = uni(C.tag[s0 + 1]), t2 = uni(C.tag[s0 + 2]), t3 = uni(C.tag[s0 + 3]);
-  if (t0 == L) return s0;
-  if (t1 == L) return s0 + 1;
-  if (t2 == L) return s0 + 2;
-  if (t3 == L) return s0 + 3;
-  int way = uni(C.rr[set]), tv = 0;
+__device__ __forceinline__ void ser_mark(unsigned long long& ne0, unsigned long long& ne1, unsigned long long& ne2,
+                                         unsigned long long& ne3, int b, bool on) {
+  const unsigned long long bit = 1ull << (b & 63);
+  const int k = b >> 6;
+  const unsigned long long m0 = k == 0 ? bit : 0ull, m1 = k == 1 ? bit : 0ull, m2 = k == 2 ? bit : 0ull,
+                           m3 = k == 3 ? bit : 0ull;
+  if (on) {
+    ne0 |= m0; ne1 |= m1; ne2 |= m2; ne3 |= m3;
+  } else {
+    ne0 &= ~m0; ne1 &= ~m1; ne2 &= ~m2; ne3 &= ~m3;
+  }
+}
+__device__ __forceinline__ unsigned long long ser_clock() {
+#ifdef MSEG_SER_PROF
+  return __builtin_amdgcn_s_memtime();
+#else
+  return 0;
+#endif
+}
+// issue the pending writes (mkb: margin-relative states; state t of a tiled pixel z is mkb[z + marg]).
+// Always nine stores, absent ones to a dummy word: vmcnt counts in issue order, and with a fixed
+// number of stores behind a pop's loads the compiler waits for the loads only (vmcnt(9 + ...)),
+// not for these stores -- with a data-dependent count it must assume none and wait for all.
+__device__ __forceinline__ void ser_flush(const Ws& ws, int* mkb, int* dummy, SerPend& P) {
+  *(P.pp >= 0 ? mkb + P.pp : dummy) = P.lab;
 #pragma unroll
-  for (int k = 0; k < SER_WAYS; ++k) {  // the first unpinned way from the round-robin pointer
-    tv = (way == 0) ? t0 : (way == 1) ? t1 : (way == 2) ? t2 : t3;
-    if (tv < 0 || (tv != pa && tv != pb)) break;
-    way = (way + 1) & (SER_WAYS - 1);
+  for (int k = 0; k < 4; ++k) {
+    const bool on = (P.m >> k) & 1u;
+    *(on ? ws.qbuf + P.qs[k] : dummy) = P.z[k] - ws.marg;
+    *(on ? mkb + P.z[k] : dummy) = P.sv[k];
   }
-  const int slot = s0 + way, lane = lane_id(), e = lane & 31;
-  // lanes 0-31 the line's states, 32-63 its weights: per-lane addresses, no branches
-  const int* src = (lane < 32) ? (mkb + L * 32 + e) : (const int*)(w4b + L * 32 + e);
-  const int v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (tv >= 0) {  // write back the victim's written entries
-    const unsigned dm = uni((int)C.dirty[slot]);
-    const int old = C.st[slot][e];
-    if (lane < 32 && ((dm >> e) & 1u)) mkb[tv * 32 + e] = old;
-  }
-  int* dst = (lane < 32) ? &C.st[slot][e] : (int*)&C.w4[slot][e];
-  *dst = v;
-  if (lane == 0) {
-    C.tag[slot] = L;
-    C.dirty[slot] = 0u;
-    C.rr[set] = (way + 1) & (SER_WAYS - 1);
-  }
-  ++fills;
-  return slot;
+  P.pp = -1;
+  P.m = 0u;
 }
 
-// every line's written entries back to global memory, two lines per step; the cache emptied
-__device__ void ser_flush(SerCache& C, int* mkb) {
-  const int lane = lane_id();
-  for (int k = 0; k < SER_LINES; k += 2) {
-    const int slot = k + (lane >> 5), e = lane & 31;
-    const int tg = C.tag[slot];
-    if (tg >= 0 && ((C.dirty[slot] >> e) & 1u)) mkb[tg * 32 + e] = C.st[slot][e];
-  }
-  wave_sync();
-  for (int k = lane; k < SER_LINES; k += 64) {
-    C.tag[k] = -1;
-    C.dirty[k] = 0u;
-  }
-  wave_sync();
-}
-
-// The pop loop of k_serial.  CACHED: the flood state through the LDS cache; otherwise straight
-// from global memory (serial_loop's accesses).  The popped bucket's next 64 queue slots are
-// prefetched into LDS, slots this launch pushed come from the per-bucket LDS rings, so a pop's
-// only global loads are line fills and prefetches.  Returns true when the cached loop gave the
-// cache up (more than 700 fills per 1024 pops): the caller flushes it and runs the rest uncached.
-struct SerRun {
-  int lo = NQ, run = 0, ring_l = -1, ring_h0 = 0, ring_n = 0;
-  long long pops = 0, pushes = 0, fills = 0;
-};
-
-template <bool CACHED>
-__device__ __forceinline__ bool ser_pops(const Ws& ws, SerCache& C, const int* s_qbase, int* s_head,
-                                                   int* s_tail, const int* s_bent, int (*s_bring)[SER_RING],
-                                                   int* s_ring, int* s_err, SerRun& R, int spec_block,
-                                                   long long cool_lim) {
+// The pop loop of k_serial; returns when the queue is empty, after SERIAL_RUN pops without an
+// interrupt (batches pay again), at the speculative engine's hand-back points, or on an error.
+// Bucket records and rings in LDS are written by lane 0 (LDS is in order within the wave).
+__device__ __forceinline__ void ser_run(const Ws& ws, int4* s_bk, int (*s_bring)[SER_RING], unsigned long long* ne,
+                                        int& err, SerStat& S, int spec_block, long long cool_lim) {
   const int lane = lane_id();
   const int Wt = ws.Wt, marg = ws.marg;
   int* const mkb = ws.mk - marg;
   const unsigned* const w4b = (const unsigned*)(ws.w4 - marg);
-  int lo = R.lo, run = R.run, ring_l = R.ring_l, ring_h0 = R.ring_h0, ring_n = R.ring_n;
-  long long pops = R.pops, pushes = R.pushes, fills = R.fills, fills0 = R.fills;
-  bool dropped = false;
-  while (lo < NQ) {
-    const int h = uni(s_head[lo]), tl = uni(s_tail[lo]), navail = tl - h;
-    if (navail <= 0) {
-      lo = lowest_bucket(s_head, s_tail, lo + 1);
-      continue;
-    }
-    if (run >= SERIAL_RUN) break;
+  unsigned long long ne0 = ne[0], ne1 = ne[1], ne2 = ne[2], ne3 = ne[3];
+  int ring = 0, ring_l = -1, ring_h0 = 0, ring_n = 0, run = 0;
+  int* const dummy = &ws.ctl->pad3;  // nobody reads it
+  SerPend P;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) P.z[k] = P.qs[k] = P.sv[k] = 0;
+  for (;;) {
+    const unsigned long long t0 = ser_clock();
+    const int lo = ne0 ? __builtin_ctzll(ne0) : ne1 ? 64 + __builtin_ctzll(ne1)
+                 : ne2 ? 128 + __builtin_ctzll(ne2) : ne3 ? 192 + __builtin_ctzll(ne3) : NQ;
+    if (lo >= NQ || run >= SERIAL_RUN) break;
     if (spec_block > 0 && lo >= spec_block) break;  // the cascade that stopped the speculative engine is done
-    if (pops >= cool_lim) break;                    // its cooldown is over
-    if (ws.spec_lazy && pops >= 4096) break;        // the engine is being allocated: let it take over
+    if (S.pops >= cool_lim) break;                  // its cooldown is over
+    if (ws.spec_lazy && S.pops >= 4096) break;      // the engine is being allocated: let it take over
+    const int4 rec = s_bk[lo];
+    const int h = uni(rec.x), tl = uni(rec.y), qb = uni(rec.z), be = uni(rec.w);
     int p;
-    if (h >= uni(s_bent[lo]) && h >= tl - SER_RING) {  // pushed by this launch: its LDS ring
+    if (h >= be && h >= tl - SER_RING) {  // pushed by this launch: its LDS ring
       p = uni(s_bring[lo][h & (SER_RING - 1)]);
-    } else {
-      if (lo != ring_l || h >= ring_h0 + ring_n) {  // the bucket's next 64 slots, one load per lane
-        ring_l = lo;
-        ring_h0 = h;
-        ring_n = min(navail, 64);
-        const int v = (lane < ring_n) ? ld_qbuf_v(ws, s_qbase[lo] + h + lane) : 0;
-        s_ring[lane] = v;
-      }
-      p = uni(s_ring[h - ring_h0]);
+    } else if (lo == ring_l && h >= ring_h0 && h < ring_h0 + ring_n) {
+      p = __builtin_amdgcn_readlane(ring, h - ring_h0);
+    } else {  // the bucket's next 64 slots, one load per lane, after the pending writes (their slots)
+      ser_flush(ws, mkb, dummy, P);
+      ring_l = lo;
+      ring_h0 = h;
+      ring_n = min(tl - h, 64);
+      ring = (lane < ring_n) ? __hip_atomic_load(ws.qbuf + qb + h + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                             : 0;
+      p = __builtin_amdgcn_readlane(ring, 0);
     }
+    const unsigned long long t1 = ser_clock();
     const int pb = p + marg;
-    int nv[4], st[4], sl[4];
+    int nv[4], st[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) nv[d] = nbi(pb, d, Wt);
-    unsigned w4;
-    int s0 = -1;
-    if (CACHED) {
-      const int L0 = pb >> 5;
-      s0 = ser_line(C, mkb, w4b, L0, -1, -1, fills);
-      int Lh = -1, sh = -1;  // the horizontal neighbour line (left or right: one at most)
 #pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        const int L = nv[d] >> 5;
-        if (L != L0) {
-          Lh = L;
-          sh = ser_line(C, mkb, w4b, L, L0, -1, fills);
-        }
-      }
-      int sv = -1;  // the vertical one (up or down)
-#pragma unroll
-      for (int d = 2; d < 4; ++d) {
-        const int L = nv[d] >> 5;
-        if (L != L0 && L != Lh) sv = ser_line(C, mkb, w4b, L, L0, Lh, fills);
-      }
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int L = nv[d] >> 5;
-        sl[d] = (L == L0) ? s0 : (L == Lh) ? sh : sv;
-        st[d] = uni(C.st[sl[d]][nv[d] & 31]);
-      }
-      w4 = (unsigned)uni((int)C.w4[s0][pb & 31]);
-    } else {
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        sl[d] = -1;
-        st[d] = uni(__hip_atomic_load(mkb + nv[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-      }
-      w4 = (unsigned)uni((int)w4b[pb]);
-    }
+    for (int d = 0; d < 4; ++d) st[d] = __hip_atomic_load(mkb + nv[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const unsigned w4r = w4b[pb];
+    // the previous pop's writes go out now, behind this pop's loads; what they change is patched below
+    SerPend Q = P;
+    ser_flush(ws, mkb, dummy, P);
+    const unsigned w4 = (unsigned)uni((int)w4r);
     int lab = 0;
 #pragma unroll
-    for (int d = 0; d < 4; ++d)
-      if (st[d] > 0) lab = fold_lab(lab, st[d]);
+    for (int d = 0; d < 4; ++d) {
+      int v = uni(st[d]);
+      if (nv[d] == Q.pp) v = Q.lab;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (((Q.m >> k) & 1u) && nv[d] == Q.z[k]) v = Q.sv[k];
+      st[d] = v;
+      if (v > 0) lab = fold_lab(lab, v);
+    }
     if (lab == 0) {  // impossible for an exact queue
-      *s_err = ERR_STATE;
+      err |= ERR_STATE;
       lab = WSHED;
     }
-    if (CACHED) {
-      C.st[s0][pb & 31] = lab;
-      C.dirty[s0] |= 1u << (pb & 31);
-    } else {
-      mkb[pb] = lab;
-    }
-    s_head[lo] = h + 1;
-    ++pops;
-    bool lower = false;
-    int newlo = lo;
+    P.pp = pb;
+    P.lab = lab;
+    if (lane == 0) s_bk[lo].x = h + 1;
+    ++S.pops;
+    const unsigned long long t2 = ser_clock();
+    bool lower = false, lo_left = h + 1 < tl;
     if (lab != WSHED) {
+      // the push targets' bucket records, all in one round trip
+      int4 tr[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) tr[d] = s_bk[(w4 >> (8 * d)) & 255u];
+      unsigned pm = 0u;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         if (st[d] != 0) continue;
         const int t = (int)((w4 >> (8 * d)) & 255u);
-        const int tt = uni(s_tail[t]);
-        const int dest = s_qbase[t] + tt;
+        int tt = uni(tr[d].y);
+        // an earlier push of this pop into the same bucket advanced its tail
+#pragma unroll
+        for (int e = 0; e < d; ++e)
+          if (st[e] == 0 && (int)((w4 >> (8 * e)) & 255u) == t) ++tt;
+        const int dest = uni(tr[d].z) + tt;
         if (dest < 0 || (long long)dest >= ws.qcap) {
-          *s_err = ERR_CAPACITY;
+          err |= ERR_CAPACITY;
           continue;
         }
-        ws.qbuf[dest] = nv[d] - marg;
-        s_bring[t][tt & (SER_RING - 1)] = nv[d] - marg;
-        if (CACHED) {
-          C.st[sl[d]][nv[d] & 31] = queued_state(dest);
-          C.dirty[sl[d]] |= 1u << (nv[d] & 31);
-        } else {
-          mkb[nv[d]] = queued_state(dest);
+        const int z = nv[d] - marg;
+        P.z[d] = nv[d];
+        P.qs[d] = dest;
+        P.sv[d] = queued_state(dest);
+        pm |= 1u << d;
+        if (lane == 0) {
+          s_bring[t][tt & (SER_RING - 1)] = z;
+          s_bk[t].y = tt + 1;
         }
-        s_tail[t] = tt + 1;
-        ++pushes;
-        if (t < lo) lower = true;
-        newlo = min(newlo, t);
+        ser_mark(ne0, ne1, ne2, ne3, t, true);
+        ++S.pushes;
+        lower = lower || t < lo;
+        lo_left = lo_left || t == lo;
       }
+      P.m = pm;
     }
+    if (!lo_left) ser_mark(ne0, ne1, ne2, ne3, lo, false);
     run = lower ? 0 : run + 1;
-    lo = newlo;
-    if (*s_err) break;
-    // a cache that misses on most pops (uniform-random frames: the flood front is everywhere at
-    // once) costs more than it saves: judged every 1024 pops
-    if (CACHED && (pops & 1023) == 0) {
-      if (fills - fills0 > 700) {
-        dropped = true;
-        break;
-      }
-      fills0 = fills;
-    }
+#ifdef MSEG_SER_PROF
+    const unsigned long long t3 = ser_clock();
+    S.tsel += t1 - t0;
+    S.tld += t2 - t1;
+    S.tpush += t3 - t2;
+#else
+    (void)t0;
+    (void)t1;
+    (void)t2;
+#endif
+    if (err) break;
   }
-  R.lo = lo;
-  R.run = run;
-  R.ring_l = ring_l;
-  R.ring_h0 = ring_h0;
-  R.ring_n = ring_n;
-  R.pops = pops;
-  R.pushes = pushes;
-  R.fills = fills;
-  return dropped;
+  ser_flush(ws, mkb, dummy, P);
 }
 
 __global__ __launch_bounds__(64) void k_serial(Ws ws, int iter) {
   Ctl* ctl = ws.ctl;
-  __shared__ SerCache C;
   __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ];
-  __shared__ int s_bent[NQ];               // bucket tails at entry: later slots were pushed here
   __shared__ int s_bring[NQ][SER_RING];    // the last SER_RING pixels pushed to each bucket
   __shared__ Seg s_seg[NQ];
-  __shared__ int s_ring[64];               // the next 64 queue slots of one bucket (prefetched)
   __shared__ int s_err, s_nseg, s_n, s_specool, s_specblk;
   const int lane = lane_id();
   const Batch B0 = ctl->bat;
   if (B0.mode == 4 && !ctl->error) {
-    for (int k = lane; k < NQ; k += 64) {
-      s_qbase[k] = ctl->qbase[k];
-      s_head[k] = ctl->qhead[k];
-      s_tail[k] = ctl->qtail[k];
-      s_bent[k] = s_tail[k];
-    }
-    for (int k = lane; k < SER_SETS; k += 64) C.rr[k] = 0;
-    for (int k = lane; k < SER_LINES; k += 64) {
-      C.tag[k] = -1;
-      C.dirty[k] = 0u;
+    __shared__ int4 s_bk[NQ];  // {head, tail, base, tail at entry} per bucket
+    __shared__ unsigned long long s_ne[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int b = 64 * k + lane;
+      const int hd = ctl->qhead[b], tl = ctl->qtail[b];
+      s_qbase[b] = ctl->qbase[b];
+      s_bk[b] = make_int4(hd, tl, s_qbase[b], tl);
+      const unsigned long long m = __ballot(tl > hd);
+      if (lane == 0) s_ne[k] = m;
     }
     if (lane == 0) {
-      s_err = 0;
       s_specblk = ws.spx ? ctl->spec.block : -1;  // -1: engine off
       s_specool = ctl->spec.cool;
     }
     wave_sync();
-    int* const mkb = ws.mk - ws.marg;
     const int spec_block = s_specblk > 0 ? s_specblk : 0;
     const long long cool_lim = (s_specblk >= 0 && s_specool > 0) ? s_specool : (1ll << 62);
-    SerRun R;
-    R.lo = lowest_bucket(s_head, s_tail, 0);
     const unsigned long long t_start = ws.diag ? __builtin_amdgcn_s_memrealtime() : 0;
-    // the cached loop, then -- if the cache kept missing -- the rest of the run without it
-    const bool dropped = ser_pops<true>(ws, C, s_qbase, s_head, s_tail, s_bent, s_bring, s_ring, &s_err, R,
-                                        spec_block, cool_lim);
-    if (dropped) {
-      ser_flush(C, mkb);
-      ser_pops<false>(ws, C, s_qbase, s_head, s_tail, s_bent, s_bring, s_ring, &s_err, R, spec_block, cool_lim);
-    } else {
-      ser_flush(C, mkb);
+    const unsigned long long c_start = ser_clock();
+    SerStat S;
+    int err = 0;
+    ser_run(ws, s_bk, s_bring, s_ne, err, S, spec_block, cool_lim);
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int4 r = s_bk[64 * k + lane];
+      s_head[64 * k + lane] = r.x;
+      s_tail[64 * k + lane] = r.y;
     }
-    const long long pops = R.pops, pushes = R.pushes, fills = R.fills;
+    if (lane == 0) s_err = err;
+    const long long pops = S.pops, pushes = S.pushes;
     if (ws.diag && lane == 0) {
       atomicAdd(&ws.diag[19], (unsigned long long)pops);
       atomicAdd(&ws.diag[20], __builtin_amdgcn_s_memrealtime() - t_start);
       atomicAdd(&ws.diag[21], 1ull);
-      atomicAdd(&ws.diag[22], (unsigned long long)fills);
+#ifdef MSEG_SER_PROF  // the per-pop phase split (scripts/serial_phases.py), in shader cycles
+      atomicAdd(&ws.diag[16], S.tsel);
+      atomicAdd(&ws.diag[17], S.tld);
+      atomicAdd(&ws.diag[18], S.tpush);
+      atomicAdd(&ws.diag[22], ser_clock() - c_start);
+#else
+      (void)c_start;
+#endif
     }
     wave_sync();
     form_batch(s_qbase, s_head, s_tail, 0, 0, s_seg, &s_nseg, &s_n);

@@ -129,7 +129,7 @@ class Segmenter:
         self._check(self._L.msg_set_fast_commit(self._h, 1 if on else 0))
 
     def set_serial_kernel(self, on=True):
-        """Serial-pop regime in k_serial with LDS-cached state (default off: inside k_scan)."""
+        """Serial-pop regime in k_serial, one wave (default off: the pops run inside k_scan)."""
         self._check(self._L.msg_set_serial_kernel(self._h, 1 if on else 0))
 
     def set_speculative(self, on=True):

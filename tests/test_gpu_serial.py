@@ -1,5 +1,5 @@
-"""GPU parity of k_serial -- the serial-pop regime in a kernel of its own with the flood state
-cached in LDS (csrc/ws_kernels.hip) -- against the CPU oracle and against serial pops inside the
+"""GPU parity of k_serial -- the serial-pop regime in a kernel of its own, queue bookkeeping in
+registers and LDS records, stores deferred behind the next pop's loads (csrc/ws_kernels.hip) -- against the CPU oracle and against serial pops inside the
 one-workgroup loop, on the inputs that live in that regime: real photographs (album.jpg pixels with
 the shape method's seeds), scattered notConnectedMarkers-like seeds, noisy frames with the
 speculative engine off (so every interrupt-dense stretch is popped serially)."""
