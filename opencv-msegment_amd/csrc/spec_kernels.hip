@@ -812,7 +812,11 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
         // resumes once the lowest level is back at L (generations inside a cascade that
         // overflowed a lane are small: measured slower)
         s.on = 0;
+#if MSEG_SPEC_NEST
+        s.block = 0;  // the regime may take the overflowing cascade's own generations over
+#else
         s.block = slow ? 0 : L;
+#endif
         s.fallbacks += 1;
         ctl->wcap = WMIN;
       } else if (Vn == P && s.n >= SPEC_QUIET) {  // a large generation without a cascade: batches pay

@@ -69,6 +69,9 @@ constexpr int ERR_LEFTOVER = 8;  // a queued (or phase-1) state survived the flo
 // changes (the serial result is the unique fixed point: item i depends only on items < i).
 constexpr int SPEC_WIN = 1 << 20;   // items per generation (claim ranks have 22 bits)
 constexpr int SPEC_BS = 256;        // threads per k_spec_round block
+#ifndef MSEG_SPEC_NEST
+#define MSEG_SPEC_NEST 0
+#endif
 #ifndef MSEG_SPEC_QCAP
 #define MSEG_SPEC_QCAP 32
 #endif
