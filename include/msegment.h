@@ -75,6 +75,11 @@ typedef struct msg_stats {
     int64_t spec_replays;       /* executions whose cascade was replayed from the previous
                                    round's log (no input changed): spec_executions - spec_replays
                                    cascades were run pop by pop                                 */
+    int64_t spec_cooldowns;     /* times the regime was judged slower than serial pops (each
+                                   followed by a stretch of serial pops)                          */
+    int64_t spec_gen_pops;      /* pops committed by generations (the rest were popped serially
+                                   or in batches)                                               */
+    int64_t spec_gen_us;        /* device time from generation starts to their flattening, us  */
 } msg_stats;
 
 #define MSG_NKERNELS 24

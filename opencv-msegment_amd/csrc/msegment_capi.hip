@@ -555,6 +555,9 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   c->stats.spec_rounds = tail.spec.rounds_total;
   c->stats.spec_executions = tail.spec.execs;
   c->stats.spec_replays = tail.spec.replays;
+  c->stats.spec_cooldowns = tail.spec.cools;
+  c->stats.spec_gen_pops = tail.spec.gpops_total;
+  c->stats.spec_gen_us = tail.spec.gticks_total / 100;  // s_memrealtime: 100 MHz
   c->stats.spec_cascade_pops = tail.spec.cpops;
   c->stats.spec_fallbacks = tail.spec.fallbacks;
   if (spec_bound) c->stag = tail.spec.T;

@@ -802,21 +802,24 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
       // every generation (fallbacks included) is judged against serial pops over the span since
       // the regime's start: slower per committed pop (small generations: a round costs launch
       // floors and its longest execution; frequent fallbacks) -> serial pops for a while
-      const long long el = (long long)__builtin_amdgcn_s_memrealtime() - s.tstart;
-      const long long done = ctl->pops + Vn - s.pstart;  // k_scan adds Vn after this kernel
+      const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+      const long long el = now - s.tstart;
+      s.gpops_total += Vn;
+      s.gticks_total += now - s.tgen;
       ++s.accg;
       const bool judge = s.accg >= SPEC_JUDGE_GENS || (s.accg >= 4 && el > SPEC_JUDGE_TICKS);
-      const bool slow = judge && el > (long long)SPEC_SERIAL_TICKS * done;
+      // judged on the generations' own time (+ a commit estimate each) per pop they committed,
+      // not on the wall time since the regime started: a fallback's serial pops cost the same
+      // either way (round 3 A/B: neutral on every frame, profiles/r03l_ab_regimes.log)
+      s.tspec += now - s.tgen + SPEC_COMMIT_TICKS;
+      s.pspec += Vn;
+      const bool slow = judge && s.tspec > (long long)SPEC_SERIAL_TICKS * s.pspec;
       if (s.fallback) {
         // the batch engine pops the overflowing item and its cascade (serial pops); the regime
         // resumes once the lowest level is back at L (generations inside a cascade that
         // overflowed a lane are small: measured slower)
         s.on = 0;
-#if MSEG_SPEC_NEST
-        s.block = 0;  // the regime may take the overflowing cascade's own generations over
-#else
         s.block = slow ? 0 : L;
-#endif
         s.fallbacks += 1;
         ctl->wcap = WMIN;
       } else if (Vn == P && s.n >= SPEC_QUIET) {  // a large generation without a cascade: batches pay
@@ -828,6 +831,7 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
         s.block = 0;
         s.cool = SPEC_COOL_POPS << min(s.fails, 6);
         s.fails += 1;
+        s.cools += 1;
         s.fresh = 1;
       }
       s.state = 0;

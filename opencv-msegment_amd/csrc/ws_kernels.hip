@@ -797,6 +797,7 @@ __device__ void spec_begin(Ctl* ctl, Batch& nb, int L, int bstart, int navail) {
   ctl->slogtop.v = 0;
   s.fallback = 0;
   s.ftile = 0;
+  s.tgen = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2595,6 +2596,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
         ctl->spec.fresh = 0;
         ctl->spec.accg = 0;
         ctl->spec.tstart = (long long)__builtin_amdgcn_s_memrealtime();
+        ctl->spec.tspec = ctl->spec.pspec = 0;
         ctl->spec.pstart = ctl->pops + nb_pops;  // nb_pops: this loop's, added below
       }
       ctl->spec.on = 1;
@@ -2899,6 +2901,7 @@ __global__ __launch_bounds__(64) void k_serial(Ws ws, int iter) {
           ctl->spec.fresh = 0;
           ctl->spec.accg = 0;
           ctl->spec.tstart = (long long)__builtin_amdgcn_s_memrealtime();
+          ctl->spec.tspec = ctl->spec.pspec = 0;
           ctl->spec.pstart = ctl->pops + pops;
         }
         ctl->spec.on = 1;

@@ -69,9 +69,6 @@ constexpr int ERR_LEFTOVER = 8;  // a queued (or phase-1) state survived the flo
 // changes (the serial result is the unique fixed point: item i depends only on items < i).
 constexpr int SPEC_WIN = 1 << 20;   // items per generation (claim ranks have 22 bits)
 constexpr int SPEC_BS = 256;        // threads per k_spec_round block
-#ifndef MSEG_SPEC_NEST
-#define MSEG_SPEC_NEST 0
-#endif
 #ifndef MSEG_SPEC_QCAP
 #define MSEG_SPEC_QCAP 32
 #endif
@@ -89,6 +86,7 @@ constexpr int SPEC_JUDGE_GENS = 16;          // slower than that per committed p
                                              // generations, ends for
 constexpr int SPEC_COOL_POPS = 65536;        // this many serial pops (doubling per repeat)
 constexpr int SPEC_JUDGE_TICKS = 200000;     // slow generations are judged after 4 once 2 ms passed
+constexpr int SPEC_COMMIT_TICKS = 3000;      // ~30 us: a generation's ordered append (k_scan, k_scatter)
 
 // A tiled pixel's speculative-generation words (k_spec_round reads a neighbour's whole record
 // with two 16-B loads).
@@ -115,9 +113,14 @@ struct SpecCtl {
   int ftile;      // k_spec_flatten tile dealing
   int cool;       // serial pops to go before the regime may start again
   int accg;       // generations since the regime started (fallback resumptions included)
-  int fails;      // times the regime ended for being slower than serial pops
+  int fails;      // consecutive times the regime ended for being slower than serial pops
+  int cools;      // all such times in this flood
   int fresh;      // the next start opens a new judging span (flood start, after such an end)
   long long tstart, pstart;  // regime start: s_memrealtime, Ctl.pops
+  long long tgen;            // s_memrealtime at the current generation's start (spec_begin)
+  long long gpops_total, gticks_total;  // whole flood: pops the generations committed, their time
+  long long tspec, pspec;    // since the regime start: generations' own time (+ a commit estimate
+                             // each) and the pops they committed -- what the regime is judged on
   long long gens, rounds_total, execs, cpops, fallbacks;
   unsigned long long rmax;  // diagnostics: longest wave of this round (10 ns ticks)
   int ov1, ov2;             // lowest overflowing rank of the last / the one-before-last round

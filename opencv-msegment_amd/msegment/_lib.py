@@ -61,7 +61,9 @@ class Stats(ctypes.Structure):
                 ("diag", ctypes.c_int64 * 8),
                 ("spec_generations", ctypes.c_int64), ("spec_rounds", ctypes.c_int64),
                 ("spec_executions", ctypes.c_int64), ("spec_cascade_pops", ctypes.c_int64),
-                ("spec_fallbacks", ctypes.c_int64), ("spec_replays", ctypes.c_int64)]
+                ("spec_fallbacks", ctypes.c_int64), ("spec_replays", ctypes.c_int64),
+                ("spec_cooldowns", ctypes.c_int64), ("spec_gen_pops", ctypes.c_int64),
+                ("spec_gen_us", ctypes.c_int64)]
 
 
 class KernelProfile(ctypes.Structure):

@@ -53,9 +53,11 @@ for name, kind, S, seed in cases:
         ok = hashlib.sha256(np.ascontiguousarray(lab).tobytes()).hexdigest() == dig[key]["labels_sha256"]
     else:
         ok = np.array_equal(lab, ws_oracle.watershed(img, m))
-    print("%%-18s %%9.1f ms  %%s  gens %%d rounds %%d execs %%d fallbacks %%d pops %%d batches %%d" %% (
+    print("%%-18s %%9.1f ms  %%s  gens %%d rounds %%d execs %%d fallbacks %%d pops %%d batches %%d | cooldowns %%d "
+          "gen pops %%d in %%.1f ms (%%.3f us/pop)" %% (
         name, statistics.median(ts), "exact" if ok else "MISMATCH", st["spec_generations"], st["spec_rounds"],
-        st["spec_executions"], st["spec_fallbacks"], st["pops"], st["batches"]), flush=True)
+        st["spec_executions"], st["spec_fallbacks"], st["pops"], st["batches"], st["spec_cooldowns"],
+        st["spec_gen_pops"], st["spec_gen_us"] / 1e3, st["spec_gen_us"] / max(1, st["spec_gen_pops"])), flush=True)
 seg.close()
 '''
 
