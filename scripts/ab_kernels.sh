@@ -7,7 +7,7 @@ OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 for rep in 1 2; do
   for lib in "$@"; do
     name=$(basename "$lib" .so)
-    MSEGMENT_LIB=$(realpath "$lib") timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/$name.$rep.log" 2>&1
+    MSEGMENT_LIB=$(realpath "$lib") timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ${AB_ARGS:-} > "$OUT/$name.$rep.log" 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "STOP $name rc=$rc"; tail -3 "$OUT/$name.$rep.log"; exit $rc; }
     python - "$OUT/$name.$rep.log" "$name" "$rep" "$K" <<'PY'
 import json, sys
