@@ -27,18 +27,13 @@ import sys
 import time
 
 # Batch mode (--frames / the "batch" object) keeps several floods in flight on their own streams;
-# the HIP runtime maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4), and streams that
-# share a queue serialise.  8 queues let 4 floods (+ torch's and the context's own stream) run side
-# by side (4 in flight at 8 queues = 7250 Mpx/s vs 5160 at 4).  Must be set before
-# HIP initialises; the GPU boxes export 4, so raise it (a larger outer setting is kept).
-try:
-    _hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
-except ValueError:
-    _hwq = 0
-if os.environ.get("MSEG_BENCH_HWQ"):  # the batch_hwq4 child: exactly this many queues
+# the HIP runtime maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4, as the GPU boxes
+# export).  Round 2 raised it to 8 here (4 in flight: 7250 Mpx/s at 8 queues against 5160 at 4);
+# on the round-3 library the default 4 queues give the same rate (batch.hwq4 8781 against 8653 Mpx/s
+# at 8, profiles/r03i_bench.json), so the bench now runs at whatever the environment sets, as a
+# library user would.  The batch_hwq4 child pins exactly MSEG_BENCH_HWQ.
+if os.environ.get("MSEG_BENCH_HWQ"):
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ["MSEG_BENCH_HWQ"]
-else:
-    os.environ["GPU_MAX_HW_QUEUES"] = str(max(_hwq, 8))
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "opencv-msegment_amd"))

@@ -12,8 +12,9 @@ for rep in 1 2; do
     python - "$OUT/$name.$rep.log" "$name" "$rep" "$K" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-k = [x for x in d["kernels"] if x["kernel"] == sys.argv[4]]
-print("%-10s rep%s value %9.2f  %s %s us  parity %s" % (sys.argv[2], sys.argv[3], d["value"], sys.argv[4], k[0]["avg_us"] if k else None, d["parity"]))
+ks = {x["kernel"]: x["avg_us"] for x in d["kernels"]}
+print("%-14s rep%s value %9.2f  %s  parity %s" % (sys.argv[2], sys.argv[3], d["value"],
+      "  ".join("%s %s us" % (k, ks.get(k)) for k in sys.argv[4].split(",")), d["parity"]))
 PY
   done
 done

@@ -99,6 +99,35 @@ def test_float_rounding_of_large_bins():
     assert O.flex_levels(h, 4)[0].count == (1 << 24) * 2 + (1 << 24) + 4
 
 
+def _without_int_wrap(monkeypatch, fn):
+    """The same oracle call with Python's unbounded ints in place of Java's 32-bit wrap."""
+    with monkeypatch.context() as mp:
+        mp.setattr(O, "_i32", lambda x: x)
+        return fn()
+
+
+def test_multi_otsu_wraps_bin_index_times_count(monkeypatch):
+    # otsuPart's `ii * intensity` (PictureService.java:958) is an int product: reduced bin 125
+    # (grey 250) holding 20 M pixels gives 2.5e9, which wraps negative in Java, and moves the
+    # thresholds (frames of >= ~17 M pixels with a bright mode reach this)
+    h = H(b10=3_000_000, b160=2_000_000, b250=20_000_000)
+    rows, cols = 1000, int(h.sum()) // 1000
+    want = [(0, 159, 3_000_000), (160, 161, 2_000_000), (162, 255, 20_000_000)]
+    assert O.levels(h, rows, cols, 4, multi_otsu_opt=True) == want
+    assert msegment.nc_levels(h, rows, cols, 4, OTSU) == want
+    assert _without_int_wrap(monkeypatch, lambda: O.levels(h, rows, cols, 4, multi_otsu_opt=True)) != want
+
+
+def test_multi_otsu_wraps_pixel_count(monkeypatch):
+    # pixNum = rows * cols (PictureService.java:656) is an int: 65536 x 32768 wraps to -2^31
+    h = np.zeros(256, np.int64)
+    h[10:20], h[30], h[200:210] = 100, 5, 50
+    want = [(0, -1, 0), (0, 255, 1505)]
+    assert O.levels(h, 65536, 32768, 4, multi_otsu_opt=True) == want
+    assert msegment.nc_levels(h, 65536, 32768, 4, OTSU) == want
+    assert _without_int_wrap(monkeypatch, lambda: O.levels(h, 65536, 32768, 4, multi_otsu_opt=True)) != want
+
+
 def _random_hist(rng, kind):
     if kind == "dense":
         h = rng.integers(0, 5000, 256)
