@@ -400,6 +400,37 @@ union Prep4Lds {
   int4 tile[4 * PREP4_T];
 };
 
+// One row of a thread's tile column as loaded: 4 BGR pixels (12 B), 4 markers, and for the two
+// halo threads the strip's outside column (x0 - 1 or x0 + RSEG).
+struct Prep4Row {
+  Quad3 q;
+  int4 m;
+  uint32_t hv;
+  int hm;
+};
+
+__device__ __forceinline__ Prep4Row prep4_load(const Ws& ws, const int32_t* __restrict__ mk_in, int r, int c0,
+                                               bool tin, bool halo, int hc) {
+  const int H = ws.H, W = ws.W;
+  Prep4Row x;
+  x.q = Quad3{0, 0, 0};
+  x.m = make_int4(0, 0, 0, 0);
+  x.hv = 0;
+  x.hm = 0;
+  if (r < 0 || r >= H) return x;
+  if (tin) {
+    const unsigned o = (unsigned)r * (unsigned)W + (unsigned)c0;
+    x.q = *reinterpret_cast<const Quad3*>(ws.img + 3u * o);
+    x.m = *reinterpret_cast<const int4*>(mk_in + o);
+  }
+  if (halo && hc >= 0 && hc < W) {
+    const unsigned o = (unsigned)r * (unsigned)W + (unsigned)hc;
+    x.hv = (uint32_t)ws.img[3u * o] | ((uint32_t)ws.img[3u * o + 1] << 8) | ((uint32_t)ws.img[3u * o + 2] << 16);
+    x.hm = mk_in[o];
+  }
+  return x;
+}
+
 __global__ __launch_bounds__(PREP4_T) void k_prep4(Ws ws, const int32_t* __restrict__ mk_in) {
   __shared__ unsigned caph[NQ];
   __shared__ Prep4Lds u;
@@ -414,19 +445,21 @@ __global__ __launch_bounds__(PREP4_T) void k_prep4(Ws ws, const int32_t* __restr
   const int r0 = tr * 4, x0 = cs * RSEG;
   const int tc = cs * PREP4_T + tid, c0 = tc * 4;
   const bool tin = c0 < W;  // W % 4 == 0: a tile is wholly inside or wholly outside
+  const bool halo = (tid == 0 || tid == PREP4_T - 1);  // the strip's halo columns x0 - 1 and x0 + RSEG
+  const int hc = (tid == 0) ? x0 - 1 : x0 + RSEG;
   for (int k = tid; k < NQ; k += PREP4_T) caph[k] = 0;
+  // every load of the strip -- its rows and the two halo threads' outside columns -- issued before
+  // the first use: one round trip (the halo columns in a branch after the rows' LDS stores were a
+  // second one: 81-84 -> 72-75 us at 4096^2, profiles/r03n_ab_prep_commit.log "tr1")
+  Prep4Row rw[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) rw[i] = prep4_load(ws, mk_in, r0 - 1 + i, c0, tin, halo, hc);
   uint32_t px[6][4];
   int mm[6][4];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    const int r = r0 - 1 + i;
-    Quad3 q{0, 0, 0};
-    int4 m4 = make_int4(0, 0, 0, 0);
-    if (tin && r >= 0 && r < H) {
-      const unsigned o = (unsigned)r * (unsigned)W + (unsigned)c0;
-      q = *reinterpret_cast<const Quad3*>(ws.img + 3u * o);
-      m4 = *reinterpret_cast<const int4*>(mk_in + o);
-    }
+    const Quad3 q = rw[i].q;
+    const int4 m4 = rw[i].m;
     px[i][0] = q.x & 0xffffffu;
     px[i][1] = (q.x >> 24) | ((q.y & 0xffffu) << 8);
     px[i][2] = (q.y >> 16) | ((q.z & 0xffu) << 16);
@@ -437,24 +470,15 @@ __global__ __launch_bounds__(PREP4_T) void k_prep4(Ws ws, const int32_t* __restr
     s_mf[i][tid + 1] = m4.x;
     s_mb[i][tid + 1] = m4.w;
   }
-  if (tid == 0 || tid == PREP4_T - 1) {  // the strip's halo columns x0 - 1 and x0 + RSEG
-    const int c = (tid == 0) ? x0 - 1 : x0 + RSEG;
+  if (halo) {
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-      const int r = r0 - 1 + i;
-      uint32_t v = 0;
-      int m = 0;
-      if (c >= 0 && c < W && r >= 0 && r < H) {
-        const unsigned o = (unsigned)r * (unsigned)W + (unsigned)c;
-        v = (uint32_t)ws.img[3u * o] | ((uint32_t)ws.img[3u * o + 1] << 8) | ((uint32_t)ws.img[3u * o + 2] << 16);
-        m = mk_in[o];
-      }
       if (tid == 0) {
-        s_pb[i][0] = v;
-        s_mb[i][0] = m;
+        s_pb[i][0] = rw[i].hv;
+        s_mb[i][0] = rw[i].hm;
       } else {
-        s_pf[i][PREP4_T + 1] = v;
-        s_mf[i][PREP4_T + 1] = m;
+        s_pf[i][PREP4_T + 1] = rw[i].hv;
+        s_mf[i][PREP4_T + 1] = rw[i].hm;
       }
     }
   }
