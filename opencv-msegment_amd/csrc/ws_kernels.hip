@@ -1783,6 +1783,9 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
   __shared__ int s_ncommit, s_flags;
   const int tid = threadIdx.x, wv = tid >> 6;
   const int Wt = ws.Wt;
+  // the bucket bases are loaded into registers before the header: a global -> LDS copy after
+  // thread 0's header branch would cost wave 0 a second round trip before the barrier
+  const int r_qb = (tid < NQ) ? ctl->qbase[tid] : 0;
   if (tid == 0) {
     const Batch B = ctl->bat;
     int ncommit;
@@ -1790,7 +1793,7 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
     s_ncommit = ncommit;
     s_B = B;
   }
-  if (tid < NQ) qb[tid] = ctl->qbase[tid];
+  if (tid < NQ) qb[tid] = r_qb;
   __syncthreads();
   const Batch B = s_B;
   const int ncommit = s_ncommit, flags = s_flags;
@@ -1873,14 +1876,24 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
   if (flags & 1) {
     const int nch = (ncommit + CH - 1) / CH;
     const bool haspartial = (ncommit % CH) != 0 && ncommit != B.n;
+    // the queue state, the window words and the batch's segments in one round trip (registers
+    // first, then LDS)
+    const int r_wcap = ctl->wcap, r_minpush = ctl->minpush, r_cut = ctl->cut;
+    int r_h = 0, r_t = 0;
     if (tid < NQ) {
-      s_head[tid] = ctl->qhead[tid];
-      s_tail[tid] = ctl->qtail[tid];
+      r_h = ctl->qhead[tid];
+      r_t = ctl->qtail[tid];
+    }
+    Seg r_sg{0, 0, 0, 0};
+    if (tid < B.nseg) r_sg = ctl->seg[tid];
+    if (tid < NQ) {
+      s_head[tid] = r_h;
+      s_tail[tid] = r_t;
       partial[tid] = 0;
     }
     if (tid == 0) {
-      s_wcap = next_wcap(ctl->wcap, B.n, ncommit, ctl->cut != NONE && ncommit == ctl->cut + 1);
-      s_minpush = ctl->minpush;
+      s_wcap = next_wcap(r_wcap, B.n, ncommit, r_cut != NONE && ncommit == r_cut + 1);
+      s_minpush = r_minpush;
     }
     __syncthreads();
     if (haspartial) {  // the cut chunk's row counts items past the cut: recount its prefix
@@ -1898,10 +1911,8 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
       dp = gpart[0][tid] + gpart[1][tid] + gpart[2][tid] + gpart[3][tid] + partial[tid];
       s_tail[tid] += dp;
     }
-    if (tid < B.nseg) {  // advance every segment's bucket head by what it committed
-      const Seg sg = ctl->seg[tid];
-      atomicAdd(&s_head[sg.L], max(0, min(ncommit - sg.rank, sg.n)));
-    }
+    if (tid < B.nseg)  // advance every segment's bucket head by what it committed
+      atomicAdd(&s_head[r_sg.L], max(0, min(ncommit - r_sg.rank, r_sg.n)));
     if (tid < NQ) {
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) dp += __shfl_xor(dp, o);
