@@ -549,7 +549,11 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   c->stats.pushes = tail.pushes;
   // when speculative generations ran, diag reports their round split instead (spec_kernels.hip)
   for (int k = 0; k < 8; ++k)
+#ifdef MSEG_CF_PROF
+    c->stats.diag[k] = (int64_t)dgv[8 + k];  // k_commit_fast's phase split (diagnostic build)
+#else
     c->stats.diag[k] = (int64_t)dgv[c->diag_bank == 2 ? 16 + k : tail.spec.gens ? 8 + k : k];
+#endif
   c->stats.host_syncs = syncs;
   c->stats.spec_generations = tail.spec.gens;
   c->stats.spec_rounds = tail.spec.rounds_total;

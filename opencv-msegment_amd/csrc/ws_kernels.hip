@@ -1785,6 +1785,15 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
   const int Wt = ws.Wt;
   // the bucket bases are loaded into registers before the header: a global -> LDS copy after
   // thread 0's header branch would cost wave 0 a second round trip before the barrier
+#ifdef MSEG_CF_PROF
+  // diagnostic build (make cfprof, scripts/cf_phases.py): s_memrealtime phase split, diag[8..15]
+  const long long cf_t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  unsigned long long* const cfd = ws.diag ? ws.diag + 8 : nullptr;
+  long long cf_t[6] = {0, 0, 0, 0, 0, 0};
+#define CF_STAMP(k) do { if (cfd && tid == 0) cf_t[k] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define CF_STAMP(k) do { } while (0)
+#endif
   const int r_qb = (tid < NQ) ? ctl->qbase[tid] : 0;
   if (tid == 0) {
     const Batch B = ctl->bat;
@@ -1795,6 +1804,7 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
   }
   if (tid < NQ) qb[tid] = r_qb;
   __syncthreads();
+  CF_STAMP(0);
   const Batch B = s_B;
   const int ncommit = s_ncommit, flags = s_flags;
   unsigned* const arrive = (unsigned*)&ctl->farrive[0];
@@ -1830,6 +1840,9 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
     if (tid < NQ) run[tid] = qt + gpart[0][tid] + gpart[1][tid] + gpart[2][tid] + gpart[3][tid];
     __syncthreads();  // this block's reads of the control block and of the rows are complete
     if (tid == 0) atomicAdd(&arrive[blockIdx.x & 7], 1u);
+#ifdef MSEG_CF_PROF
+    if (cfd && tid == 0 && blockIdx.x == 0) atomicAdd(&cfd[6], (unsigned long long)((long long)__builtin_amdgcn_s_memrealtime() - cf_t0));
+#endif
 #pragma unroll
     for (int k = 0; k < SUBS - 1; ++k) {  // pushes of the earlier sub-rounds of this chunk
       const unsigned m = (unsigned)(dj[k] >> 32) & 15u;
@@ -1867,6 +1880,10 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
       st_state(ws, n, queued_state(dest));
       ws.qbuf[dest] = (int32_t)n;
     }
+#ifdef MSEG_CF_PROF
+    __syncthreads();
+    if (cfd && tid == 0 && blockIdx.x == 0) atomicAdd(&cfd[7], (unsigned long long)((long long)__builtin_amdgcn_s_memrealtime() - cf_t0));
+#endif
     return;
   }
   // ---- the finalizer ----
@@ -1896,6 +1913,7 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
       s_minpush = r_minpush;
     }
     __syncthreads();
+    CF_STAMP(1);
     if (haspartial) {  // the cut chunk's row counts items past the cut: recount its prefix
       for (int i = (nch - 1) * CH + tid; i < ncommit; i += 1024) {
         const unsigned long long d = ws.desc[i];
@@ -1920,6 +1938,7 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
     }
     __syncthreads();
     form_batch(qb, s_head, s_tail, s_minpush, s_wcap, nsegs, &s_nseg, &s_n);
+    CF_STAMP(2);
   }
   // wait for every sub-round block's arrival -- each arrives once it has read the control block,
   // whether or not it has a sub-round to scatter (a block starting after the finalizer wrote would
@@ -1943,6 +1962,7 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
       }
     }
     if (tid < 8) arrive[tid] = 0u;  // every arrival is in: reset for the next launch
+    CF_STAMP(3);
   }
   __syncthreads();
   if (flags & 1) {
@@ -1988,6 +2008,17 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
       if (ns > 0) ctl->batches += 1;
       else ctl->done = 1;
     }
+#ifdef MSEG_CF_PROF
+    CF_STAMP(4);
+    if (cfd && tid == 0) {  // header, queue-state loads, rows + segments + next batch, arrivals, writes
+      atomicAdd(&cfd[0], (unsigned long long)(cf_t[0] - cf_t0));
+      atomicAdd(&cfd[1], (unsigned long long)(cf_t[1] - cf_t[0]));
+      atomicAdd(&cfd[2], (unsigned long long)(cf_t[2] - cf_t[1]));
+      atomicAdd(&cfd[3], (unsigned long long)(cf_t[3] - cf_t[2]));
+      atomicAdd(&cfd[4], (unsigned long long)(cf_t[4] - cf_t[3]));
+      atomicAdd(&cfd[5], 1ull);
+    }
+#endif
   } else if (tid == 0) {
     if (flags & 2) {
       ctl->rgive = 0;
