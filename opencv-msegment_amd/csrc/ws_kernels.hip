@@ -1608,15 +1608,13 @@ __device__ __forceinline__ void wave_rank(unsigned mask, unsigned lvls, int pos[
 #pragma unroll
     for (int d = 0; d < 4; ++d)
       if (((rem >> d) & 1u) && (int)((lvls >> (8 * d)) & 255u) == lsel) sel |= 1u << d;
+    // exclusive prefix of the per-lane counts (0..4) from three ballots of their bits and
+    // mbcnt (lanes below this one), instead of a six-step shuffle scan: no LDS-crossbar round
+    // trips on the ordered append's critical path
     const int cnt = __popc(sel);
-    int x = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    const int total = __shfl(x, 63);
-    int k = x - cnt;
+    const unsigned long long b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
+    const int total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+    int k = lanes_below(b0) + 2 * lanes_below(b1) + 4 * lanes_below(b2);
 #pragma unroll
     for (int d = 0; d < 4; ++d)
       if ((sel >> d) & 1u) pos[d] = k++;
@@ -1880,10 +1878,6 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
       st_state(ws, n, queued_state(dest));
       ws.qbuf[dest] = (int32_t)n;
     }
-#ifdef MSEG_CF_PROF
-    __syncthreads();
-    if (cfd && tid == 0 && blockIdx.x == 0) atomicAdd(&cfd[7], (unsigned long long)((long long)__builtin_amdgcn_s_memrealtime() - cf_t0));
-#endif
     return;
   }
   // ---- the finalizer ----
@@ -1924,6 +1918,7 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
     }
     gpart[tid >> 8][tid & (NQ - 1)] = rows_sum(ws.cnt, tid >> 8, haspartial ? nch - 1 : nch, tid & (NQ - 1));
     __syncthreads();
+    CF_STAMP(5);
     int dp = 0;
     if (tid < NQ) {
       dp = gpart[0][tid] + gpart[1][tid] + gpart[2][tid] + gpart[3][tid] + partial[tid];
@@ -2013,10 +2008,11 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
     if (cfd && tid == 0) {  // header, queue-state loads, rows + segments + next batch, arrivals, writes
       atomicAdd(&cfd[0], (unsigned long long)(cf_t[0] - cf_t0));
       atomicAdd(&cfd[1], (unsigned long long)(cf_t[1] - cf_t[0]));
-      atomicAdd(&cfd[2], (unsigned long long)(cf_t[2] - cf_t[1]));
-      atomicAdd(&cfd[3], (unsigned long long)(cf_t[3] - cf_t[2]));
-      atomicAdd(&cfd[4], (unsigned long long)(cf_t[4] - cf_t[3]));
-      atomicAdd(&cfd[5], 1ull);
+      atomicAdd(&cfd[2], (unsigned long long)(cf_t[5] - cf_t[1]));  // rows (+ a cut chunk's recount)
+      atomicAdd(&cfd[3], (unsigned long long)(cf_t[2] - cf_t[5]));  // segments, next batch
+      atomicAdd(&cfd[4], (unsigned long long)(cf_t[3] - cf_t[2]));
+      atomicAdd(&cfd[5], (unsigned long long)(cf_t[4] - cf_t[3]));
+      atomicAdd(&cfd[7], 1ull);
     }
 #endif
   } else if (tid == 0) {

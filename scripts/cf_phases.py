@@ -2,8 +2,8 @@
 headline frame.  Needs the diagnostic build (make -C opencv-msegment_amd/csrc cfprof):
 MSEGMENT_LIB=.../libmsegment_cfprof.so python scripts/cf_phases.py
 The finalizer block's thread 0 stamps s_memrealtime (100 MHz) after the batch header, the queue
-state, the rows + segments + next batch, the wait for every sub-round block's arrival and the
-queue-state writes; sub-round block 0 stamps its arrival and its end.  Averages per committed
+state, the histogram rows, the segments + next batch, the wait for every sub-round block's
+arrival and the queue-state writes; sub-round block 0 stamps its arrival.  Averages per committed
 launch, in microseconds from each block's own first instruction."""
 import os
 import sys
@@ -30,11 +30,12 @@ def main():
         seg.watershed_dev(t_img, t_m, t_lab)
         torch.cuda.synchronize()
         d = seg.stats()["diag"]
-        n = max(1, d[5])
+        n = max(1, d[7])
         us = [x / n / 100.0 for x in d]
-        print("rep %d: %d committed launches; finalizer: header %.2f, queue state %.2f, rows+segs+next batch %.2f, "
-              "arrivals %.2f, writes %.2f (sum %.2f us); sub-round block 0: arrival %.2f, end %.2f us"
-              % (rep, d[5], us[0], us[1], us[2], us[3], us[4], sum(us[:5]), us[6], us[7]), flush=True)
+        print("rep %d: %d committed launches; finalizer: header %.2f, queue state %.2f, rows %.2f, "
+              "segments + next batch %.2f, arrivals %.2f, writes %.2f (sum %.2f us); sub-round block 0 "
+              "arrives at %.2f us" % (rep, d[7], us[0], us[1], us[2], us[3], us[4], us[5], sum(us[:6]), us[6]),
+              flush=True)
 
 
 if __name__ == "__main__":
