@@ -51,6 +51,30 @@ __device__ __forceinline__ int lanes_below(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
 }
 
+// Wave-wide scans and reductions in DPP lane moves (row_shr 1/2/4/8 within each 16-lane row, then
+// row_bcast 15/31 across rows): six VALU steps instead of six LDS-crossbar shuffles
+// (ds_bpermute, ~50+ cycles each on a dependent chain).  The whole wave must be active.
+__device__ __forceinline__ int wave_scan_add(int v) {  // inclusive
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+__device__ __forceinline__ int wave_sum(int v) { return __builtin_amdgcn_readlane(wave_scan_add(v), 63); }
+__device__ __forceinline__ int wave_min(int v) {
+  constexpr int MAXI = 0x7fffffff;
+  v = min(v, __builtin_amdgcn_update_dpp(MAXI, v, 0x111, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(MAXI, v, 0x112, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(MAXI, v, 0x114, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(MAXI, v, 0x118, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(MAXI, v, 0x142, 0xa, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(MAXI, v, 0x143, 0xc, 0xf, false));
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
 __device__ __forceinline__ unsigned long long ld_granule(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -351,12 +375,11 @@ __global__ __launch_bounds__(RSEG) void k_prep(Ws ws, const int32_t* __restrict_
   // the chunk's raster offset in qbuf (read by k_compact; qbuf is filled only after it):
   // segmented exclusive scan, row ry's count in bits 16*ry of a 64-bit word ----
   const unsigned long long mine = (unsigned long long)__popc(p1mask) << (16 * ry);
-  unsigned long long x = mine;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
+  // the four 16-bit row counts never carry into each other (at most 4 per lane, 64 lanes), so the
+  // 64-bit scan is two 32-bit DPP scans
+  const unsigned long long x =
+      (unsigned long long)(uint32_t)wave_scan_add((int)(uint32_t)mine) |
+      ((unsigned long long)(uint32_t)wave_scan_add((int)(uint32_t)(mine >> 32)) << 32);
   if (lane == 63) s_wsum[wv] = x;
   __syncthreads();
   unsigned long long excl = x - mine, total = 0;
@@ -569,12 +592,11 @@ __global__ __launch_bounds__(PREP4_T) void k_prep4(Ws ws, const int32_t* __restr
   unsigned long long mine = 0;
 #pragma unroll
   for (int ry = 0; ry < 4; ++ry) mine |= (unsigned long long)__popc(p1m[ry]) << (16 * ry);
-  unsigned long long x = mine;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
+  // the four 16-bit row counts never carry into each other (at most 4 per lane, 64 lanes), so the
+  // 64-bit scan is two 32-bit DPP scans
+  const unsigned long long x =
+      (unsigned long long)(uint32_t)wave_scan_add((int)(uint32_t)mine) |
+      ((unsigned long long)(uint32_t)wave_scan_add((int)(uint32_t)(mine >> 32)) << 32);
   if (lane == 63) s_wsum[wv] = x;
   __syncthreads();
   unsigned long long excl = x - mine, total = 0;
@@ -669,8 +691,7 @@ __device__ void column_scan(const int* cnt, int* coff, int nch, const int* parti
 __device__ int block_sum(int v) {  // every thread of the block calls; result to all
   __shared__ int part[32];
   const int nw = (blockDim.x + 63) >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  v = wave_sum(v);
   if (lane_id() == 0) part[threadIdx.x >> 6] = v;
   __syncthreads();
   int r = 0;
@@ -702,17 +723,8 @@ __device__ void form_batch(const int* qbase, const int* head, const int* tail, i
       lo = min(lo, l);
     }
   }
-  int xe = ne, xs = sum;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int ye = __shfl_up(xe, o), ys = __shfl_up(xs, o);
-    if (lane >= o) {
-      xe += ye;
-      xs += ys;
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) lo = min(lo, __shfl_xor(lo, o));
+  const int xe = wave_scan_add(ne), xs = wave_scan_add(sum);
+  lo = wave_min(lo);
   const bool merge = minpush > lo;
   int segi = xe - ne, cum = xs - sum, inc_n = 0, inc_items = 0;
 #pragma unroll
@@ -733,11 +745,8 @@ __device__ void form_batch(const int* qbase, const int* head, const int* tail, i
     cum += cnt[k];
     ++segi;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    inc_n += __shfl_xor(inc_n, o);
-    inc_items += __shfl_xor(inc_items, o);
-  }
+  inc_n = wave_sum(inc_n);
+  inc_items = wave_sum(inc_items);
   if (lane == 0) {
     *nseg_out = inc_n;
     *n_out = inc_items;
@@ -1528,8 +1537,7 @@ __device__ Batch scan_body(const Ws& ws) {
   column_scan(ws.cnt, ws.coff, nch, haspartial ? partial : nullptr, s_tail);
   if (tid < NQ) {  // pushes appended: one atomic per wave of levels (no block barrier)
     int dp = s_tail[tid] - oldt;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) dp += __shfl_xor(dp, o);
+    dp = wave_sum(dp);
     if ((tid & 63) == 0 && dp) atomicAdd((unsigned long long*)&ctl->pushes, (unsigned long long)dp);
   }
   if (B.mode == 0 && tid < B.nseg) {  // advance every segment's bucket head by what it committed
@@ -1584,8 +1592,7 @@ __device__ Batch scan_body(const Ws& ws) {
     int q = 0;
 #pragma unroll
     for (int k = 0; k < NQ / 64; ++k) q += s_tail[tid + 64 * k] - s_head[tid + 64 * k];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    q = wave_sum(q);
     if (tid == 0) ctl->remaining = q;
   }
   __syncthreads();
@@ -1927,8 +1934,7 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
     if (tid < B.nseg)  // advance every segment's bucket head by what it committed
       atomicAdd(&s_head[r_sg.L], max(0, min(ncommit - r_sg.rank, r_sg.n)));
     if (tid < NQ) {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) dp += __shfl_xor(dp, o);
+      dp = wave_sum(dp);
       if ((tid & 63) == 0 && dp) atomicAdd((unsigned long long*)&ctl->pushes, (unsigned long long)dp);
     }
     __syncthreads();
@@ -1974,8 +1980,7 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
       int q = 0;
 #pragma unroll
       for (int k = 0; k < NQ / 64; ++k) q += s_tail[tid + 64 * k] - s_head[tid + 64 * k];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+      q = wave_sum(q);
       if (tid == 0) ctl->remaining = q;
     }
     if (tid == 0) {
@@ -2165,11 +2170,8 @@ __device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qba
     const unsigned long long lowmask = __ballot(lower);
     const int cut = lowmask ? (__ffsll((long long)lowmask) - 1) : NONE;
     int minpush = lower ? 0 : tmin, segcut = mseg;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      minpush = min(minpush, __shfl_xor(minpush, o));
-      segcut = min(segcut, __shfl_xor(segcut, o));
-    }
+    minpush = wave_min(minpush);
+    segcut = wave_min(segcut);
     int ncommit = B.n;
     if (cut != NONE) ncommit = min(ncommit, cut + 1);
     if (segcut != NONE) ncommit = min(ncommit, s_seg[segcut].rank);
@@ -2213,8 +2215,7 @@ __device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qba
         if ((int)((it.wts >> (8 * d)) & 255u) == lsel) rem &= ~(1u << d);
       wave_sync();
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) pushed += __shfl_xor(pushed, o);
+    pushed = wave_sum(pushed);
     if (lane < B.nseg) {
       const Seg s = s_seg[lane];
       s_head[s.L] += max(0, min(ncommit - s.rank, s.n));
@@ -2279,9 +2280,7 @@ __device__ __forceinline__ int lowest_bucket(const int* head, const int* tail, i
     const int l = lane * (NQ / 64) + k;
     if (l >= from && tail[l] > head[l]) lo = min(lo, l);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) lo = min(lo, __shfl_xor(lo, o));
-  return lo;
+  return wave_min(lo);
 }
 
 __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qbase, int* s_head, int* s_tail,
@@ -2313,7 +2312,7 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
       ring_n = min(navail, 64);
       ring = (lane < ring_n) ? ld_qbuf_v(ws, s_qbase[lo] + h + lane) : 0;
     }
-    const int p = __shfl(ring, h - ring_h0);
+    const int p = __builtin_amdgcn_readlane(ring, h - ring_h0);  // a uniform lane: no LDS crossbar
     const int pb = p + marg;
     int nb[4], st[4];
 #pragma unroll
@@ -2944,8 +2943,7 @@ __global__ __launch_bounds__(64) void k_serial(Ws ws, int iter) {
     int q = 0;
 #pragma unroll
     for (int k = 0; k < NQ / 64; ++k) q += s_tail[lane + 64 * k] - s_head[lane + 64 * k];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    q = wave_sum(q);
     if (lane == 0) {
       Batch nb;
       nb.mode = 0;
