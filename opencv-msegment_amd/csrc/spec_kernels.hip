@@ -239,7 +239,7 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
     // (pre-checking the word with a load before the atomic, sharding the log counter per
     // blockIdx % 8 and skipping rank-minimum atomics already beaten measured 26% slower)
     if (lane == 0) r0 = atomicAdd(&ctl->sdeal.v, 64);
-    r0 = __shfl(r0, 0);
+    r0 = __builtin_amdgcn_readlane(r0, 0);
     if (r0 >= n) break;
     const int j = r0 + lane;
     // ---- promote: final since the last round; their claims become permanent ----
@@ -574,16 +574,11 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
     }
     // ---- log space for the wave's records (one atomic per wave), signatures, change words ----
     const int want = (ex && !ovf && rbase < 0) ? nrec : 0;
-    int incl = want;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(incl, o);
-      if (lane >= o) incl += y;
-    }
-    const int wtot = __shfl(incl, 63);
+    const int incl = wave_scan_add(want);
+    const int wtot = __builtin_amdgcn_readlane(incl, 63);
     int wbase = 0;
     if (lane == 0 && wtot) wbase = atomicAdd(&ctl->slogtop.v, wtot);
-    wbase = __shfl(wbase, 0);
+    wbase = __builtin_amdgcn_readlane(wbase, 0);
     int fcand = NONE, ocand = NONE;
     if (ex) {
       const int base = rbase >= 0 ? rbase : wbase + incl - want;
@@ -618,11 +613,8 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
           for (int k = 0; k < pr.y; ++k) mark(ws.slog[pr.x + k]);
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      fcand = min(fcand, __shfl_xor(fcand, o));
-      ocand = min(ocand, __shfl_xor(ocand, o));
-    }
+    fcand = wave_min(fcand);
+    ocand = wave_min(ocand);
     if (lane == 0) {
       // ranks are dealt in increasing order: once a lower rank is in, later waves skip the atomic
       if (fcand != NONE) atomicMin(&ctl->sfc.v, fcand);
@@ -726,12 +718,7 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
         rc = make_int2(r4.x, r4.y);
       }
     }
-    int x = rc.y;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
+    const int x = wave_scan_add(rc.y);
     if (lane == 63) wsum[wv] = x;
     __syncthreads();
     int excl = x - rc.y, tot = 0;

@@ -1610,7 +1610,7 @@ __device__ __forceinline__ void wave_rank(unsigned mask, unsigned lvls, int pos[
     if (act == 0) break;
     const int leader = __ffsll((long long)act) - 1;
     const int myl = rem ? (int)((lvls >> (8 * (__ffs(rem) - 1))) & 255u) : -1;
-    const int lsel = __shfl(myl, leader);
+    const int lsel = __builtin_amdgcn_readlane(myl, leader);  // uniform lane: no LDS crossbar
     unsigned sel = 0;
 #pragma unroll
     for (int d = 0; d < 4; ++d)
@@ -1952,7 +1952,7 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
       unsigned v = (tid < 8) ? __hip_atomic_load(&arrive[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
 #pragma unroll
       for (int o = 4; o > 0; o >>= 1) v += __shfl_xor(v, o);
-      v = __shfl(v, 0);
+      v = __builtin_amdgcn_readlane(v, 0);
       if ((int)v >= expect) break;
       __builtin_amdgcn_s_sleep(1);
       const long long now = (long long)__builtin_amdgcn_s_memrealtime();
@@ -2205,7 +2205,7 @@ __device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qba
       if (act == 0) break;
       const int leader = __ffsll((long long)act) - 1;
       const int myl = rem ? (int)((it.wts >> (8 * (__ffs(rem) - 1))) & 255u) : -1;
-      const int lsel = __shfl(myl, leader);
+      const int lsel = __builtin_amdgcn_readlane(myl, leader);  // uniform lane: no LDS crossbar
       if (lane == leader) {
         s_tail[lsel] += wrow[lsel];
         wrow[lsel] = 0;
