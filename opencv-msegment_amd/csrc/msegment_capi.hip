@@ -490,7 +490,10 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
           LAUNCH(c, KID_RESOLVE, st, k_resolve<true>, dim3(gres), dim3(RBS), 0, ws);
         else
           LAUNCH(c, KID_RESOLVE, st, k_resolve<false>, dim3(gres), dim3(RBS), 0, ws);
-        LAUNCH(c, KID_COMMIT_FAST, st, k_commit_fast, dim3(FAST_SUBS + 1), dim3(1024), 0, ws, it);
+        if (c->h_mir[6] == 2)  // the last report was a batch above FAST_CH chunks
+          LAUNCH(c, KID_COMMIT_FAST, st, k_commit_fast_mp, dim3(FAST_SUBS + 1), dim3(1024), 0, ws, it);
+        else
+          LAUNCH(c, KID_COMMIT_FAST, st, k_commit_fast, dim3(FAST_SUBS + 1), dim3(1024), 0, ws, it);
         continue;
       }
       if (spec_it) {

@@ -754,9 +754,12 @@ __device__ void form_batch(const int* qbase, const int* head, const int* tail, i
 }
 
 // A batch the two-launch iterations (k_resolve -> k_commit_fast) suit: a flood batch too large
-// for k_scan's one-workgroup loop, and within k_commit_fast's chunk limit.
-__device__ __forceinline__ bool fast_batch(const Batch& b) {
-  return b.mode == 0 && b.n > SMALL_MAX && b.n <= FAST_CH * CH;
+// for k_scan's one-workgroup loop, and within k_commit_fast's chunk limit: 1 within FAST_CH chunks
+// (k_commit_fast), 2 within FAST_PASS * FAST_CH (k_commit_fast_mp), 0 otherwise.  A batch the
+// commit declined (hold) is k_scan's: 0, so that the host goes back to three-launch iterations.
+__device__ __forceinline__ int fast_batch(const Batch& b, const Ctl* ctl) {
+  if (b.mode != 0 || b.n <= SMALL_MAX || ctl->hold == b.epoch) return 0;
+  return b.n <= FAST_CH * CH ? 1 : b.n <= FAST_PASS * FAST_CH * CH ? 2 : 0;
 }
 
 // rank -> segment (segments sorted by rank); slot -> batch rank or -1 (sorted by bstart too:
@@ -1721,7 +1724,7 @@ __global__ __launch_bounds__(1024) void k_scatter(Ws ws, int iter) {
     __hip_atomic_store(ws.hmir + 3, ws.ctl->remaining, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 4, ws.ctl->spec.on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 5, ws.ctl->spec_want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(ws.hmir + 6, fast_batch(ws.ctl->bat) ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 6, fast_batch(ws.ctl->bat, ws.ctl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 7, ws.ctl->bat.mode == 4 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -1762,9 +1765,18 @@ __device__ __forceinline__ int rows_sum(const int* cnt, int g, int nrows, int lv
   for (int k = 0; k < FAST_CH / 4; ++k) sum += v[k];
   return sum;
 }
+// the same over any number of rows, FAST_CH rows (one round trip) at a time
+__device__ __forceinline__ int rows_sum_any(const int* cnt, int g, int nrows, int lv) {
+  int sum = 0;
+#pragma unroll 1
+  for (int c0 = 0; c0 < nrows; c0 += FAST_CH)
+    sum += rows_sum(cnt + (long long)c0 * NQ, g, min(FAST_CH, nrows - c0), lv);
+  return sum;
+}
 
 // What the commit of the current batch is: 1 commit ncommit items, 2 re-run (a k_resolve block
 // gave its chunk up), 4 decided but too large (k_scan commits it), 0 nothing to do.
+template <bool MP>
 __device__ __forceinline__ int fast_flags(const Ctl* ctl, const Batch& B, int& ncommit) {
   const unsigned rsv = ctl->rsv, hold = ctl->hold;
   const int err = ctl->error, give = ctl->rgive, cut = ctl->cut, segcut = ctl->segcut;
@@ -1772,17 +1784,19 @@ __device__ __forceinline__ int fast_flags(const Ctl* ctl, const Batch& B, int& n
   const bool decided = B.mode == 0 && B.n > 0 && rsv == B.epoch && !err && hold != B.epoch;
   if (!decided) return 0;
   if (give) return 2;
-  if (B.n > FAST_CH * CH) return 4;
+  if (B.n > (MP ? FAST_PASS : 1) * FAST_CH * CH) return 4;
   ncommit = B.n;
   if (cut != NONE) ncommit = min(ncommit, cut + 1);
   if (segcut != NONE) ncommit = min(ncommit, ctl->seg[segcut].rank);
   return 1;
 }
 
-__global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
+template <bool MP>
+__device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
+  constexpr int NPASS = MP ? FAST_PASS : 1;
   Ctl* ctl = ws.ctl;
   constexpr int NW = 16, SUBS = CH / 1024;
-  __shared__ int run[NQ], qb[NQ], gpart[4][NQ];
+  __shared__ int run[NQ], qb[NQ], gpart[4][NQ], s_run[NPASS][NQ];
   __shared__ int wcnt[NW][NQ];
   __shared__ Batch s_B;
   __shared__ int s_ncommit, s_flags;
@@ -1803,7 +1817,7 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
   if (tid == 0) {
     const Batch B = ctl->bat;
     int ncommit;
-    s_flags = fast_flags(ctl, B, ncommit);
+    s_flags = fast_flags<MP>(ctl, B, ncommit);
     s_ncommit = ncommit;
     s_B = B;
   }
@@ -1820,70 +1834,95 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
       if (tid == 0) atomicAdd(&arrive[blockIdx.x & 7], 1u);
       return;
     }
-    // everything this block reads, issued together (one round trip): the earlier sub-rounds'
-    // descriptors of its chunk, its own items, the old tails, the earlier chunks' histogram rows
-    const int sub = vb % SUBS;
-    unsigned long long dj[SUBS - 1];
-#pragma unroll
-    for (int k = 0; k < SUBS - 1; ++k) dj[k] = (k < sub) ? ws.desc[ch * CH + k * 1024 + tid] : 0ull;
-    const int i = i0 + tid;
-    const bool valid = i < ncommit;
-    unsigned long long dself = 0;
-    int pself = 0, lself = 0;
-    if (valid) {
-      dself = ws.desc[i];
-      pself = ws.ipx[i];
-      lself = (int)(uint32_t)ws.tl[i];
+    // Sub-rounds vb, vb + FAST_SUBS, ... (up to FAST_PASS of them: batches of up to FAST_PASS *
+    // FAST_CH chunks).  First, for each of them, everything the finalizer will rewrite -- the old
+    // tails and the earlier chunks' histogram rows -- is read and reduced to the sub-round's
+    // starting offsets per level (s_run); then the block arrives, and the scatters follow (their
+    // descriptors, items and granules are the batch's, which only the next k_resolve rewrites).
+    // pass j's chunk is FAST_CH chunks after pass j - 1's: its row prefix adds one window of
+    // FAST_CH rows (one round trip) to the previous one
+    int acc = (tid < NQ) ? ctl->qtail[tid] : 0;
+    int npass = 0;
+#pragma unroll 1
+    for (int j = 0; j < NPASS; ++j) {
+      const int vs = vb + j * FAST_SUBS, chj = vs / SUBS;
+      if (chj * CH + (vs % SUBS) * 1024 >= ncommit) break;  // block-uniform
+      const int c0 = (j == 0) ? 0 : chj - FAST_CH;
+      gpart[tid >> 8][tid & (NQ - 1)] = rows_sum(ws.cnt + (long long)c0 * NQ, tid >> 8, chj - c0, tid & (NQ - 1));
+      __syncthreads();
+      if (tid < NQ) {
+        acc += gpart[0][tid] + gpart[1][tid] + gpart[2][tid] + gpart[3][tid];
+        s_run[j][tid] = acc;
+      }
+      __syncthreads();
+      ++npass;
     }
-    const int qt = (tid < NQ) ? ctl->qtail[tid] : 0;
-    gpart[tid >> 8][tid & (NQ - 1)] = rows_sum(ws.cnt, tid >> 8, ch, tid & (NQ - 1));
-    if (tid < NQ) {
-#pragma unroll
-      for (int k = 0; k < NW; ++k) wcnt[k][tid] = 0;
-    }
-    __syncthreads();
-    if (tid < NQ) run[tid] = qt + gpart[0][tid] + gpart[1][tid] + gpart[2][tid] + gpart[3][tid];
-    __syncthreads();  // this block's reads of the control block and of the rows are complete
+    // this block's reads of the control block and of the rows are complete
     if (tid == 0) atomicAdd(&arrive[blockIdx.x & 7], 1u);
 #ifdef MSEG_CF_PROF
     if (cfd && tid == 0 && blockIdx.x == 0) atomicAdd(&cfd[6], (unsigned long long)((long long)__builtin_amdgcn_s_memrealtime() - cf_t0));
 #endif
+#pragma unroll 1
+    for (int j = 0; j < npass; ++j) {
+      const int vs = vb + j * FAST_SUBS, chj = vs / SUBS, sub = vs % SUBS;
+      const int i0j = chj * CH + sub * 1024;
+      // the earlier sub-rounds' descriptors of its chunk and its own items: one round trip
+      unsigned long long dj[SUBS - 1];
 #pragma unroll
-    for (int k = 0; k < SUBS - 1; ++k) {  // pushes of the earlier sub-rounds of this chunk
-      const unsigned m = (unsigned)(dj[k] >> 32) & 15u;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if ((m >> e) & 1u) atomicAdd(&run[(dj[k] >> (8 * e)) & 255], 1);
-    }
-    const unsigned mask = (unsigned)(dself >> 32) & 15u;
-    const unsigned lvls = (unsigned)dself;
-    const long long p = pself;
-    if (valid) st_state(ws, p, lself);
-    int pos[4] = {0, 0, 0, 0};
-    wave_rank(mask, lvls, pos, wcnt[wv]);
-    __syncthreads();
-    if (tid < NQ) {
-      int acc = run[tid];
-#pragma unroll
-      for (int k = 0; k < NW; ++k) {
-        const int t = wcnt[k][tid];
-        wcnt[k][tid] = acc;
-        acc += t;
+      for (int k = 0; k < SUBS - 1; ++k) dj[k] = (k < sub) ? ws.desc[chj * CH + k * 1024 + tid] : 0ull;
+      const int i = i0j + tid;
+      const bool valid = i < ncommit;
+      unsigned long long dself = 0;
+      int pself = 0, lself = 0;
+      if (valid) {
+        dself = ws.desc[i];
+        pself = ws.ipx[i];
+        lself = (int)(uint32_t)ws.tl[i];
       }
-    }
-    __syncthreads();
+      if (tid < NQ) {
+        run[tid] = s_run[j][tid];
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      if (!((mask >> d) & 1u)) continue;
-      const int lv = (lvls >> (8 * d)) & 255;
-      const int dest = qb[lv] + wcnt[wv][lv] + pos[d];
-      if (dest < 0 || (long long)dest >= ws.qcap) {
-        atomicOr(&ctl->error, ERR_CAPACITY);
-        continue;
+        for (int k = 0; k < NW; ++k) wcnt[k][tid] = 0;
       }
-      const long long n = nb_of(p, d, Wt);
-      st_state(ws, n, queued_state(dest));
-      ws.qbuf[dest] = (int32_t)n;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < SUBS - 1; ++k) {  // pushes of the earlier sub-rounds of this chunk
+        const unsigned m = (unsigned)(dj[k] >> 32) & 15u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if ((m >> e) & 1u) atomicAdd(&run[(dj[k] >> (8 * e)) & 255], 1);
+      }
+      const unsigned mask = (unsigned)(dself >> 32) & 15u;
+      const unsigned lvls = (unsigned)dself;
+      const long long p = pself;
+      if (valid) st_state(ws, p, lself);
+      int pos[4] = {0, 0, 0, 0};
+      wave_rank(mask, lvls, pos, wcnt[wv]);
+      __syncthreads();
+      if (tid < NQ) {
+        int acc = run[tid];
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+          const int t = wcnt[k][tid];
+          wcnt[k][tid] = acc;
+          acc += t;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        if (!((mask >> d) & 1u)) continue;
+        const int lv = (lvls >> (8 * d)) & 255;
+        const int dest = qb[lv] + wcnt[wv][lv] + pos[d];
+        if (dest < 0 || (long long)dest >= ws.qcap) {
+          atomicOr(&ctl->error, ERR_CAPACITY);
+          continue;
+        }
+        const long long n = nb_of(p, d, Wt);
+        st_state(ws, n, queued_state(dest));
+        ws.qbuf[dest] = (int32_t)n;
+      }
+      __syncthreads();  // wcnt / run are reused by the next pass
     }
     return;
   }
@@ -1923,7 +1962,9 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
           if ((m >> k) & 1u) atomicAdd(&partial[(d >> (8 * k)) & 255], 1);
       }
     }
-    gpart[tid >> 8][tid & (NQ - 1)] = rows_sum(ws.cnt, tid >> 8, haspartial ? nch - 1 : nch, tid & (NQ - 1));
+    const int nrows = haspartial ? nch - 1 : nch;
+    gpart[tid >> 8][tid & (NQ - 1)] = MP ? rows_sum_any(ws.cnt, tid >> 8, nrows, tid & (NQ - 1))
+                                         : rows_sum(ws.cnt, tid >> 8, nrows, tid & (NQ - 1));
     __syncthreads();
     CF_STAMP(5);
     int dp = 0;
@@ -2036,10 +2077,19 @@ __global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) {
     __hip_atomic_store(ws.hmir + 3, ctl->remaining, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 4, ctl->spec.on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 5, ctl->spec_want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(ws.hmir + 6, fast_batch(nb) ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 6, fast_batch(nb, ctl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 7, nb.mode == 4 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+// batches of up to FAST_CH chunks (the common case: 46-54 VGPRs, two blocks per CU)
+__global__ __launch_bounds__(1024) void k_commit_fast(Ws ws, int iter) { commit_fast_body<false>(ws, iter); }
+// up to FAST_PASS * FAST_CH chunks (large frames' generations: 16384^2 peaks at ~700 K items),
+// each sub-round block taking several sub-rounds; held to 64 VGPRs so that two blocks per CU keep
+// the whole grid resident (it spills some: only launched when the last report was such a batch)
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_commit_fast_mp(Ws ws, int iter) {
+  commit_fast_body<true>(ws, iter);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2990,7 +3040,7 @@ __global__ __launch_bounds__(64) void k_serial(Ws ws, int iter) {
     __hip_atomic_store(ws.hmir + 3, ctl->remaining, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 4, ctl->spec.on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 5, ctl->spec_want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(ws.hmir + 6, fast_batch(nb) ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 6, fast_batch(nb, ctl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 7, nb.mode == 4 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }

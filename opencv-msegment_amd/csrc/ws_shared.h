@@ -22,8 +22,9 @@ constexpr int SMALL_MAX = 4096;    // batches up to this size run in k_scan's on
 constexpr int PAL_LDS_MAX = 16384; // palettes up to this many labels are staged in LDS
 constexpr int MERGE_CAP = 1 << 22; // largest multi-segment batch (items)
 constexpr int WMIN = 64;           // smallest batch window (one wave: the tiny-batch loop)
-constexpr int FAST_CH = 120;       // k_commit_fast: batches of at most FAST_CH chunks of CH items
-                                   // (4 FAST_CH + 1 blocks of 1024 threads: resident at 2 per CU)
+constexpr int FAST_CH = 120;       // k_commit_fast: 4 FAST_CH + 1 blocks of 1024 threads (resident
+                                   // at 2 per CU), each sub-round block taking up to FAST_PASS
+constexpr int FAST_PASS = 4;       // 1024-item sub-rounds: batches of up to FAST_PASS * FAST_CH chunks
 // Batch window after committing ncommit of n items: an interrupt cut (a push below the item's
 // level) means the queue order is turning over fast, so the next batch is a short prefix; a
 // batch that filled its window uncut quadruples it.  Prefixes of the queue order: exact.
