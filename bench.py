@@ -52,10 +52,15 @@ BYTES_PER_PIXEL = {"k_prep": 15.0, "k_untile": 11.0, "k_colorize": 7.0, "k_edge_
 # k_resolve per item: queue entry 4 + own weights 4 + 4 neighbour states 16, out ipx 4 + granule 8
 # + desc 8 (push-competitor reads are data dependent and not counted)
 BYTES_PER_ITEM = {"k_resolve": 44.0}        # per batch item resolved
-# k_spec_round per execution (one item's top pop; cascade pops are data dependent, not counted):
-# queue entry 4 + own weights 4 + 4 neighbour states 16 in, claim 8 + label 4 + record 8 out
+# k_spec_round per pop it executes, top pops and cascade pops alike: queue entry 4 + own weights 4
+# + 4 neighbour states 16 in, claim 8 + label 4 + record 8 out.  Executed pops = the executions
+# (top pops) + the cascade pops they ran = executions x (pops per committed execution), i.e.
+# spec_executions * spec_gen_pops / committed executions; the engine counts committed pops, so the
+# per-round cascade pops are estimated from the committed ratio (round 3 left them out).
 BYTES_PER_EXEC = {"k_spec_round": 44.0}
-# k_serial per serial pop: queue entry 4 + own weights 4 + 4 neighbour states 16 in, label 4 out
+# k_scatter and k_commit_fast: per committed item 24 B (descriptor 8 + pixel 4 + granule 8 in,
+# state 4 out), per appended push 8 B (queue slot 4 + state 4 out); each over the items that path
+# committed (msg_stats fast_* / scatter_*)
 BYTES_SCATTER = (24.0, 8.0)                 # per committed item, per appended push
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")  # scripts/pmc_summary.py output
 E2E_BYTES_PER_PIXEL = 14.0                  # 3 B BGR + 4 B markers in, 4 B labels + 3 B BGR out
@@ -129,9 +134,16 @@ def kernel_roofline(prof, stats_per_step, npx, steps):
         elif name in BYTES_PER_ITEM:
             alg = BYTES_PER_ITEM[name] * stats_per_step["items"] * steps
         elif name in BYTES_PER_EXEC:
-            alg = BYTES_PER_EXEC[name] * stats_per_step["spec_executions"] * steps or None
+            ex = stats_per_step["spec_executions"]
+            gens_items = max(1, stats_per_step["spec_gen_pops"] - stats_per_step["spec_cascade_pops"])
+            pops_per_exec = stats_per_step["spec_gen_pops"] / gens_items  # 1 + cascade pops per item
+            alg = BYTES_PER_EXEC[name] * ex * pops_per_exec * steps or None
         elif name == "k_scatter":
-            alg = (BYTES_SCATTER[0] * stats_per_step["pops"] + BYTES_SCATTER[1] * stats_per_step["pushes"]) * steps
+            alg = (BYTES_SCATTER[0] * stats_per_step["scatter_pops"]
+                   + BYTES_SCATTER[1] * stats_per_step["scatter_pushes"]) * steps or None
+        elif name == "k_commit_fast":
+            alg = (BYTES_SCATTER[0] * stats_per_step["fast_pops"]
+                   + BYTES_SCATTER[1] * stats_per_step["fast_pushes"]) * steps or None
         else:
             alg = None
         avg_us = 1000.0 * total_ms / launches
@@ -139,7 +151,8 @@ def kernel_roofline(prof, stats_per_step, npx, steps):
         rows.append({"kernel": name, "launches_per_step": launches / steps, "avg_us": round(avg_us, 3),
                      "total_ms_per_step": round(total_ms / steps, 4),
                      "alg_bytes_per_launch": (alg / launches) if alg else None,
-                     "achieved_gbs": round(gbs, 2) if gbs else None})
+                     "achieved_gbs": round(gbs, 2) if gbs else None,
+                     "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None})
     rows.sort(key=lambda r: -r["total_ms_per_step"])
     return rows
 
@@ -261,17 +274,26 @@ def batch_throughput(seg, args, S, seed, sync, steps=5, warmup=2):
         seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)
     sync()
     dt = time.perf_counter() - t0
+    # every frame of the timed batch against its committed oracle digest, where there is one
+    dgs = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
+    checked = bad = 0
+    for k in range(K):
+        key = "%s_%dx%d_s%d" % (args.kind, S, S, seed + k)
+        if key in dgs:
+            checked += 1
+            bad += hashlib.sha256(labs[k].cpu().numpy().tobytes()).hexdigest() != dgs[key]["labels_sha256"]
+    parity = ("%d/%d frames bit-exact vs oracle digests" % (checked - bad, checked)) if checked else None
     del imgs, mks, labs, dsts
     return {"value": round(K * S * S * steps / dt / 1e6, 3), "unit": "Mpx/s", "frames": K,
-            "inflight": min(K, args.inflight), "steps": steps,
+            "inflight": min(K, args.inflight), "steps": steps, "parity": parity,
             "note": "BASELINE config 5 per GPU: %d frames (seeds %d..%d) per call, floods overlapped"
                     % (K, seed, seed + K - 1)}
 
 
 def batch_hwq4(args, S, seed):
-    """The batch line as a library user at the boxes' default of GPU_MAX_HW_QUEUES=4 gets it (this
-    process raised its own to 8 before HIP started): a child process with exactly 4 queues runs
-    the same batch at 2, 3 and 4 floods in flight."""
+    """The batch line pinned to GPU_MAX_HW_QUEUES=4 (the boxes' default; this process runs at
+    whatever the environment sets): a child process with exactly 4 queues runs the same batch at
+    2, 3 and 4 floods in flight."""
     import subprocess
 
     out = None
@@ -346,6 +368,80 @@ def cpu_baseline_batch(kind, S, seed, K):
     return {"value": round(K * S * S / dt / 1e6, 3), "unit": "Mpx/s", "cores": nt, "kind": "port",
             "sample": "%d %s %dx%d frames (seeds %d..%d), one frame per thread: oracle/ws_oracle.c "
                       "watershed + colorize, %.1f s" % (K, kind, S, S, seed, seed + K - 1, dt)}
+
+
+def many_floods_line(seg, sync, dev, K, S=1024, steps=2, cpu=True, nc_depth=4):
+    """The reference's real call pattern for the flood: many floods whose seeds put cv::watershed's
+    exact order in its serial regime -- notConnectedMarkers' scattered seeds (PictureService.java:852,
+    90 times per image from CorrelationTestService.java:84-86, 141).  K frames (mosaic+noise SxS,
+    seeds 100..100+K-1), their NC markers from the GPU marker stage (GISTO_DIAP, depth nc_depth;
+    outside the timed region), then per step ONE batch call of all K floods + colorByIndexes in the
+    many-floods mode (msg_set_batch_floods 1: one k_serial_multi launch, one wave per flood).
+    Beside it: the default batch path (the full engine per flood, 4 in flight) on the first 8
+    frames, and the C oracle on 8 threads over all K frames, whose labels are the parity check."""
+    import numpy as np
+    import torch
+
+    from msegment import synth
+
+    fr = [synth.frame("mosaic_noise", S, S, 100 + k)[0] for k in range(K)]
+    imgs = [torch.from_numpy(f).to(dev) for f in fr]
+    mks = [torch.empty((S, S), dtype=torch.int32, device=dev) for _ in fr]
+    depth = 1
+    for t_img, t_m in zip(imgs, mks):
+        depth = max(depth, len(seg.nc_marker_stage_dev(t_img, nc_depth, t_m, 1)))  # GISTO_DIAP
+    sync()
+    labs = [torch.empty_like(m) for m in mks]
+    dsts = [torch.empty((S, S, 3), dtype=torch.uint8, device=dev) for _ in fr]
+    seg.set_batch_floods(1)
+    try:
+        seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)  # warm-up (workspaces)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)
+        sync()
+        dt = time.perf_counter() - t0
+    finally:
+        seg.set_batch_floods(0)
+    st = seg.stats()
+    out = {"workload": "%d notConnectedMarkers floods (mosaic_noise %dx%d seeds 100..%d, GISTO_DIAP depth %d "
+                       "markers) + colorByIndexes per batch call, device-resident, many-floods mode"
+                       % (K, S, S, 99 + K, nc_depth),
+           "value": round(K * S * S * steps / dt / 1e6, 3), "unit": "Mpx/s", "steps": steps,
+           "ms_per_step": round(1000.0 * dt / steps, 3), "pops_per_step": st["pops"]}
+    # the default batch path on the first 8 frames (the full engine per flood, 4 streams in flight)
+    k8 = min(8, K)
+    seg.set_batch_inflight(4)
+    t0 = time.perf_counter()
+    seg.watershed_colorize_batch_dev(imgs[:k8], mks[:k8], labs[:k8], depth, None, dsts[:k8])
+    sync()
+    out["default_batch_path"] = {"value": round(k8 * S * S / (time.perf_counter() - t0) / 1e6, 3),
+                                 "unit": "Mpx/s", "frames": k8, "inflight": 4}
+    if cpu:
+        from concurrent.futures import ThreadPoolExecutor
+
+        from oracle import ws_oracle
+
+        nt = batch_cpu_threads(K)
+        m_host = [m.cpu().numpy() for m in mks]
+
+        def one(k):
+            lab = ws_oracle.watershed(fr[k], m_host[k])
+            ws_oracle.colorize(lab, depth, None)
+            return lab
+
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(nt) as ex:
+            want = list(ex.map(one, range(K)))
+        cdt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(K * S * S / cdt / 1e6, 3), "unit": "Mpx/s", "cores": nt,
+                               "kind": "port", "sample": "the same %d floods (the GPU's markers), one frame "
+                               "per thread: oracle/ws_oracle.c watershed + colorize, %.1f s" % (K, cdt)}
+        bad = sum(not np.array_equal(labs[k].cpu().numpy(), want[k]) for k in range(K))
+        out["parity"] = "%d/%d frames bit-exact vs the C oracle" % (K - bad, K)
+    del imgs, mks, labs, dsts
+    return out
 
 
 def stress_line(seg, S, sync, dev, steps, cpu=True, kind="mosaic_noise", seed=2):
@@ -542,6 +638,8 @@ def main(argv=None):
     ap.add_argument("--nc-options", default="GISTO_DIAP", help="comma list: GISTO_DIAP,MULTI_OTSU")
     ap.add_argument("--stress-steps", type=int, default=5,
                     help="steps of the config-3 stress line (mosaic+noise at --size); 0 = skip")
+    ap.add_argument("--many-frames", type=int, default=64,
+                    help="frames of the many-floods line (0: skip it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile-pass", action="store_true")
     ap.add_argument("--batch-only", action="store_true", help=argparse.SUPPRESS)
@@ -693,6 +791,10 @@ def main(argv=None):
         if rank == 0 and world == 1 and not args.no_hwq4:
             batch["hwq4"] = batch_hwq4(args, S, bseed)
 
+    many = None
+    if rank == 0 and world == 1 and K == 1 and not MARKERS and args.kind == "mosaic" and args.many_frames > 0:
+        many = many_floods_line(seg, sync, dev, args.many_frames, cpu=not args.no_cpu_baseline)
+
     stress = stress_random = None
     if rank == 0 and world == 1 and K == 1 and not MARKERS and args.kind == "mosaic" and args.stress_steps > 0:
         stress = stress_line(seg, S, sync, dev, args.stress_steps, cpu=not args.no_cpu_baseline)
@@ -765,6 +867,7 @@ def main(argv=None):
             "batch": batch,
             "stress": stress,
             "stress_random": stress_random,
+            "many_floods": many,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
             "e2e_hbm": {"achieved": round(e2e_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

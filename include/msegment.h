@@ -48,7 +48,7 @@ extern "C" {
 #define MSG_ERANGE   (-6)  /* output array too small / search space beyond what the
                               reference could finish (documented per entry point)          */
 
-#define MSG_ABI_VERSION 4
+#define MSG_ABI_VERSION 5
 
 typedef struct msg_ctx msg_ctx;
 
@@ -80,9 +80,13 @@ typedef struct msg_stats {
     int64_t spec_gen_pops;      /* pops committed by generations (the rest were popped serially
                                    or in batches)                                               */
     int64_t spec_gen_us;        /* device time from generation starts to their flattening, us  */
+    /* where the committed items went (the per-kernel algorithmic bytes of bench.py's roofline) */
+    int64_t fast_pops, fast_pushes;        /* committed / appended by k_commit_fast             */
+    int64_t scatter_pops, scatter_pushes;  /* committed / appended through k_scan + k_scatter
+                                              (batches above 4096 items, phase 1, generations) */
 } msg_stats;
 
-#define MSG_NKERNELS 24
+#define MSG_NKERNELS 25
 typedef struct msg_kernel_profile {
     char    name[32];       /* kernel name, e.g. "k_resolve"                                   */
     int64_t launches;       /* launches timed since the last reset                              */
@@ -99,6 +103,10 @@ int  msg_create(msg_ctx** out, int device_ordinal, unsigned flags);
 void msg_destroy(msg_ctx* ctx);
 const char* msg_last_error(const msg_ctx* ctx);
 int  msg_abi_version(void);
+/* Identity of the sources the library was built from: the first 16 hex digits of the SHA-256 of
+ * csrc's sources and this header (opencv-msegment_amd/csrc/Makefile).  The Python binding refuses
+ * a library whose id differs from the sources next to it (a stale build would test old kernels). */
+const char* msg_build_id(void);
 int  msg_get_stats(const msg_ctx* ctx, msg_stats* out);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around every kernel launch
@@ -159,6 +167,19 @@ int msg_watershed_batch(msg_ctx* ctx, int n, const uint8_t* const* bgr, const si
 
 /* Floods kept in flight by the batch entry points (1..8, default 4; 1 = back to back). */
 int msg_set_batch_inflight(msg_ctx* ctx, int k);
+
+/* Many floods per launch in the batch entry points (msg_watershed_batch,
+ * msg_watershed_colorize_batch_dev), for frames whose exact flood is serial-bound -- photographs,
+ * the scattered seeds of notConnectedMarkers (PictureService.java:852, called 90 times per image by
+ * CorrelationTestService.java:84-86, 141): every frame of the call gets a workspace of its own
+ * (~44 B/px of HBM each), and ONE kernel pops all of them, one wave per flood, so the call keeps
+ * as many floods in flight as it has frames instead of msg_set_batch_inflight's streams.
+ *   mode 0: off (default: the full engine per flood, msg_set_batch_inflight of them at a time);
+ *   mode 1: every flood popped serially to its end in that kernel;
+ *   mode 2: a flood that pops 4096 times in a row without pushing below its level (a plateau,
+ *           where batches pay) is finished by the full engine instead.
+ * Results are identical in every mode (each is cv::watershed's exact serial order). */
+int msg_set_batch_floods(msg_ctx* ctx, int mode);
 
 /* Blocks per launch of the flood's decision kernel (0 = default: one wave of the device's
  * occupancy).  A performance knob only: its rank chunks are dealt in dispatch order, so any

@@ -54,7 +54,8 @@ struct msg_ctx {
   long long spec_np = 0, spec_logcap = 0;
   SpecPx* d_spx = nullptr;       // per tiled pixel: both parities' claims and labels, final claim
   unsigned long long *d_stl = nullptr, *d_slog = nullptr;
-  unsigned long long *d_ssig = nullptr, *d_stmp = nullptr, *d_sflag = nullptr;
+  unsigned long long *d_ssig = nullptr, *d_stmp = nullptr, *d_sflag = nullptr, *d_sxp = nullptr;
+  long long spec_xcap = 0;       // d_sxp entries (k_spec_round's per-round chunk pool)
   int4* d_srec = nullptr;
   int2* d_sfrec = nullptr;
   unsigned* d_sdirt = nullptr;
@@ -93,6 +94,14 @@ struct msg_ctx {
   // latency-bound), created on first use
   int inflight = 4;
   std::vector<msg_ctx*> subs;
+  // many-floods batches (msg_set_batch_floods): one workspace per frame of the call, the Ws array
+  // k_serial_multi reads, and the per-flood "still running" flags it leaves
+  int many = 0;                  // 0 off, 1 every flood serial to the end, 2 hand back to batches
+  std::vector<msg_ctx*> msubs;
+  Ws* d_wss = nullptr;
+  int wss_cap = 0;
+  uint8_t* d_mstage = nullptr;   // host-buffer many-floods batches: every frame's image + markers
+  long long mstage_cap = 0;
   // marker stage: device histogram + its pinned host mirror, gray scratch
   int cus = 0;
   unsigned* d_hist = nullptr;  // 256 bins
@@ -127,7 +136,7 @@ namespace {
 enum KernelId { KID_PREP, KID_INIT_SCAN, KID_COMPACT, KID_RESOLVE, KID_SCAN, KID_SCATTER,
                 KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_GRAY_HIST, KID_NC_MARKERS, KID_SPEC_ROUND,
                 KID_GRAY, KID_MEDIAN, KID_CANNY, KID_CCL, KID_RING, KID_NUMBER, KID_HOLES, KID_SPEC_FLATTEN,
-                KID_COLOR, KID_BILATERAL, KID_COMMIT_FAST, KID_SERIAL };
+                KID_COLOR, KID_BILATERAL, KID_COMMIT_FAST, KID_SERIAL, KID_SERIAL_MULTI };
 const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_compact", "k_resolve",
                                                 "k_scan", "k_scatter", "k_colorize",
                                                 "k_edge_weights", "k_untile", "k_gray_hist",
@@ -135,7 +144,7 @@ const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_comp
                                                 "k_median", "k_canny_nms", "k_ccl", "k_ring_median3",
                                                 "k_cc_number", "k_holes", "k_spec_flatten",
                                                 "k_color_stage", "k_bilateral", "k_commit_fast",
-                                                "k_serial"};
+                                                "k_serial", "k_serial_multi"};
 
 hipEvent_t pool_event(msg_ctx* c) {
   if (c->evused == c->evpool.size()) {
@@ -235,7 +244,8 @@ void free_flood(msg_ctx* c) {
 void free_spec(msg_ctx* c) {
   dfree(c->d_spx); dfree(c->d_stl); dfree(c->d_slog); dfree(c->d_ssig);
   dfree(c->d_stmp); dfree(c->d_sflag); dfree(c->d_srec); dfree(c->d_sfrec); dfree(c->d_sdirt);
-  c->spec_np = c->spec_logcap = 0;
+  dfree(c->d_sxp);
+  c->spec_np = c->spec_logcap = c->spec_xcap = 0;
   c->stag = 0;
 }
 
@@ -259,6 +269,10 @@ int ensure_spec(msg_ctx* c, long long np, long long n, hipStream_t st) {
     HIPCHK(c, hipMalloc((void**)&c->d_sfrec, (size_t)SPEC_WIN * sizeof(int2)));
     HIPCHK(c, hipMalloc((void**)&c->d_stmp, slots * SPEC_RL * 8));
     HIPCHK(c, hipMalloc((void**)&c->d_sflag, (size_t)(SPEC_WIN / SPEC_FT + 2) * 8));
+    // a round's cold cascade queues and long executions' records (8 B each): a pool of 2 per
+    // tiled pixel, at least 2^24 (an exhausted pool is a capacity overflow: serial pops, exact)
+    c->spec_xcap = std::max<long long>(1ll << 24, 2 * np);
+    HIPCHK(c, hipMalloc((void**)&c->d_sxp, c->spec_xcap * 8));
     c->spec_np = np;
     c->spec_logcap = logcap;
   }
@@ -365,15 +379,44 @@ int wait_progress(msg_ctx* c, hipStream_t st, int target) {
   }
 }
 
-// The exact flood on device buffers, in the context's tiled workspace, then the row-major label
-// map into d_labels (may alias d_mk_in) fused with the colourisation when d_dst is given.
-int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t* d_labels, int H,
-              int W, hipStream_t st, int depth = 0, const uint8_t* d_pal = nullptr,
-              uint8_t* d_dst = nullptr, uint8_t* d_gray = nullptr) {
+// A flood in progress on a context: its kernel arguments and the host loop's regime flags.
+struct FloodRun {
+  Ws ws;
+  int H = 0, W = 0;
+  long long N = 0, ntiled = 0;
+  bool spec = false, spec_bound = false;
+  hipStream_t st = nullptr;
+};
+
+void bind_spec(msg_ctx* c, FloodRun& fr, bool on) {
+  Ws& ws = fr.ws;
+  ws.spx = on ? c->d_spx : nullptr; ws.stl = on ? c->d_stl : nullptr;
+  ws.slog = on ? c->d_slog : nullptr; ws.srec = on ? c->d_srec : nullptr;
+  ws.ssig = on ? c->d_ssig : nullptr; ws.sfrec = on ? c->d_sfrec : nullptr;
+  ws.stmp = on ? c->d_stmp : nullptr; ws.sflag = on ? c->d_sflag : nullptr;
+  ws.sdirt = on ? c->d_sdirt : nullptr;
+  ws.sxp = on ? c->d_sxp : nullptr;
+  ws.sxcap = on ? std::min<long long>(c->spec_xcap, 0x7fffffffll) : 0;
+  ws.snp = on ? c->spec_np : 0;
+  ws.slogcap = on ? c->spec_logcap : 0;
+  ws.spec_lazy = (fr.spec && !on) ? 1 : 0;
+}
+
+// The exact flood on device buffers, in the context's tiled workspace: flood_begin sets it up and
+// queues phase 1 (k_prep .. k_scatter), flood_loop runs the host loop of iterations until the
+// flood is done, flood_end writes the row-major label map into d_labels (may alias d_mk_in) fused
+// with the colourisation when d_dst is given, and reads the counters back.  run_flood = all three;
+// the many-floods batch (batch_many) runs k_serial_multi between the first two.
+int flood_begin(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int H, int W, hipStream_t st,
+                FloodRun& fr, bool multi = false) {
   const long long N = (long long)H * W;
   c->stats = msg_stats{};
   c->stats.rows = H;
   c->stats.cols = W;
+  fr.H = H;
+  fr.W = W;
+  fr.N = N;
+  fr.st = st;
   if (N == 0) return MSG_OK;
   int rc = ensure_flood(c, H, W, st);
   if (rc) return rc;
@@ -382,7 +425,8 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
     HIPCHK(c, hipMemsetAsync(c->d_cflag, 0, (size_t)(c->cap_n / RBS + 2) * 16, st));
     c->epoch = 1;
   }
-  Ws ws;
+  Ws& ws = fr.ws;
+  ws = Ws{};
   ws.img = d_img;
   c->d_px = c->d_px_base + tile_margin(W);
   ws.mk = c->d_px;
@@ -404,6 +448,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
 
   ws.hmir = c->d_mir;
   ws.serk = c->serk ? 1 : 0;
+  ws.multi = multi ? 1 : 0;
   ws.H = H;
   ws.W = W;
   ws.Wt = (W + 3) / 4;
@@ -415,27 +460,16 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   // workspace (~64 B/px) is allocated lazily: only once a flood of this context has entered the
   // interrupt-dense (serial-pop) regime, which k_scan reports through the progress mirror; smooth
   // frames never pay for it.  From then on it is kept (msg_set_speculative(ctx, 0) frees it).
-  const long long ntiled = (long long)((H + 3) / 4) * ws.Wt * 16;
-  const bool spec = c->spec && ntiled <= (1ll << 28) && H >= 3 && W >= 3;
-  auto bind_spec = [&](bool on) {
-    ws.spx = on ? c->d_spx : nullptr; ws.stl = on ? c->d_stl : nullptr;
-    ws.slog = on ? c->d_slog : nullptr; ws.srec = on ? c->d_srec : nullptr;
-    ws.ssig = on ? c->d_ssig : nullptr; ws.sfrec = on ? c->d_sfrec : nullptr;
-    ws.stmp = on ? c->d_stmp : nullptr; ws.sflag = on ? c->d_sflag : nullptr;
-    ws.sdirt = on ? c->d_sdirt : nullptr;
-    ws.snp = on ? c->spec_np : 0;
-    ws.slogcap = on ? c->spec_logcap : 0;
-    ws.spec_lazy = (spec && !on) ? 1 : 0;
-  };
-  bool spec_bound = false;
-  if (spec && c->spec_np > 0) {  // allocated by an earlier flood: (re)size and arm it now
-    rc = ensure_spec(c, ntiled, N, st);
+  fr.ntiled = (long long)((H + 3) / 4) * ws.Wt * 16;
+  fr.spec = c->spec && !multi && fr.ntiled <= (1ll << 28) && H >= 3 && W >= 3;
+  fr.spec_bound = false;
+  if (fr.spec && c->spec_np > 0) {  // allocated by an earlier flood: (re)size and arm it now
+    rc = ensure_spec(c, fr.ntiled, N, st);
     if (rc) return rc;
-    spec_bound = true;
+    fr.spec_bound = true;
   }
-  bind_spec(spec_bound);
+  bind_spec(c, fr, fr.spec_bound);
   const int npx = (int)((N + CH - 1) / CH);
-  const int gres = std::max(1, std::min(c->res_grid, (int)((N + RBS - 1) / RBS)));
   const int gsc = std::min(npx * (CH / 1024), 1024);
   HIPCHK(c, hipMemsetAsync(c->d_ctl, 0, sizeof(Ctl), st));
   HIPCHK(c, hipMemsetAsync(c->d_capp, 0, (size_t)CAP_SLOTS * NQ * 4, st));
@@ -452,7 +486,19 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
   LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, -1);
   HIPCHK(c, hipGetLastError());
+  return MSG_OK;
+}
 
+int flood_loop(msg_ctx* c, FloodRun& fr) {
+  if (fr.N == 0) return MSG_OK;
+  Ws& ws = fr.ws;
+  ws.multi = 0;  // from here on the full engine, small-batch loop included
+  hipStream_t st = fr.st;
+  const long long N = fr.N;
+  const int npx = (int)((N + CH - 1) / CH);
+  const int gres = std::max(1, std::min(c->res_grid, (int)((N + RBS - 1) / RBS)));
+  const int gsc = std::min(npx * (CH / 1024), 1024);
+  int rc = MSG_OK;
   // Host loop: groups of iterations, one group always queued ahead.  Progress comes from the
   // host-mapped mirror that each iteration's k_scatter writes (no copy kernel, no event wait):
   // after queueing a group the host spins until the previous group's last iteration reported.
@@ -472,7 +518,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   constexpr int SPEC_ITER_ROUNDS = 3;
   const int gflat = std::max(1, c->cus);
   for (;;) {
-    const bool spec_it = spec_bound && c->h_mir[4] != 0;
+    const bool spec_it = fr.spec_bound && c->h_mir[4] != 0;
     // two-launch iterations while the last report was a large flood batch (k_commit_fast)
     const bool fast_it = !spec_it && c->fast && c->h_mir[6] != 0;
     const bool ser_it = !spec_it && c->serk && c->h_mir[7] != 0;
@@ -512,17 +558,23 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
     HIPCHK(c, hipGetLastError());
     if (prev_end >= 0) {
       rc = wait_progress(c, st, prev_end);
-      if (rc) return rc;
+      if (rc) {  // iterations are still queued: let them drain before the context is reused
+        (void)hipStreamSynchronize(st);
+        return rc;
+      }
       ++syncs;
       if (c->h_mir[1] || c->h_mir[2]) break;
-      if (spec && !spec_bound && c->h_mir[5]) {
+      if (fr.spec && !fr.spec_bound && c->h_mir[5]) {
         // first entry into the serial regime: allocate the engine; launches from here on carry it
         // (the zero fills are stream-ordered after the iterations already queued, which run
         // without it, and before the first launch that may use it)
-        rc = ensure_spec(c, ntiled, N, st);
-        if (rc) return rc;
-        spec_bound = true;
-        bind_spec(true);
+        rc = ensure_spec(c, fr.ntiled, N, st);
+        if (rc) {  // queued iterations still write the shared progress mirror: drain them first
+          (void)hipStreamSynchronize(st);
+          return rc;
+        }
+        fr.spec_bound = true;
+        bind_spec(c, fr, true);
       }
       // fewer queued items -> fewer batches left: shrink the group so that the iterations
       // enqueued past the end of the flood (no-ops, but each still a launch) stay few
@@ -531,6 +583,16 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
     }
     prev_end = it - 1;
   }
+  c->stats.host_syncs += syncs;
+  return MSG_OK;
+}
+
+int flood_end(msg_ctx* c, FloodRun& fr, int32_t* d_labels, int depth = 0, const uint8_t* d_pal = nullptr,
+              uint8_t* d_dst = nullptr, uint8_t* d_gray = nullptr) {
+  if (fr.N == 0) return MSG_OK;
+  Ws& ws = fr.ws;
+  hipStream_t st = fr.st;
+  const int H = fr.H, W = fr.W;
   {
     const long long nrows = (long long)((H + 3) / 4) * ws.Wt * 4;  // one tile row per lane
     const int grid = (int)std::min<long long>((nrows + 255) / 256, 1 << 20);
@@ -544,12 +606,16 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   unsigned long long dgv[24] = {0};
   if (c->diag) HIPCHK(c, hipMemcpyAsync(dgv, c->d_diag, sizeof(dgv), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
-  ++syncs;
+  c->stats.host_syncs += 1;
   if (c->prof) collect_profile(c);
   c->stats.batches = tail.batches;
   c->stats.pops = tail.pops;
   c->stats.items = tail.items;
   c->stats.pushes = tail.pushes;
+  c->stats.fast_pops = tail.fpops;
+  c->stats.fast_pushes = tail.fpushes;
+  c->stats.scatter_pops = tail.spops;
+  c->stats.scatter_pushes = tail.spushes;
   // when speculative generations ran, diag reports their round split instead (spec_kernels.hip)
   for (int k = 0; k < 8; ++k)
 #ifdef MSEG_CF_PROF
@@ -557,7 +623,6 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
 #else
     c->stats.diag[k] = (int64_t)dgv[c->diag_bank == 2 ? 16 + k : tail.spec.gens ? 8 + k : k];
 #endif
-  c->stats.host_syncs = syncs;
   c->stats.spec_generations = tail.spec.gens;
   c->stats.spec_rounds = tail.spec.rounds_total;
   c->stats.spec_executions = tail.spec.execs;
@@ -567,7 +632,7 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   c->stats.spec_gen_us = tail.spec.gticks_total / 100;  // s_memrealtime: 100 MHz
   c->stats.spec_cascade_pops = tail.spec.cpops;
   c->stats.spec_fallbacks = tail.spec.fallbacks;
-  if (spec_bound) c->stag = tail.spec.T;
+  if (fr.spec_bound) c->stag = tail.spec.T;
   c->epoch += (unsigned)std::min<long long>(tail.batches + 4, 0x7fffffff);
   if (tail.error & ERR_TIMEOUT)
     return fail(c, MSG_ETIMEOUT, "in-kernel wait timed out (grid not co-resident?)");
@@ -587,6 +652,17 @@ int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t*
   if (tail.error) return fail(c, MSG_ESTATE, "device consistency check failed (%d)", tail.error);
   if (!tail.done) return fail(c, MSG_ESTATE, "flood did not finish");
   return MSG_OK;
+}
+
+int run_flood(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int32_t* d_labels, int H,
+              int W, hipStream_t st, int depth = 0, const uint8_t* d_pal = nullptr,
+              uint8_t* d_dst = nullptr, uint8_t* d_gray = nullptr) {
+  FloodRun fr;
+  int rc = flood_begin(c, d_img, d_mk_in, H, W, st, fr);
+  if (rc) return rc;
+  rc = flood_loop(c, fr);
+  if (rc) return rc;
+  return flood_end(c, fr, d_labels, depth, d_pal, d_dst, d_gray);
 }
 
 int launch_colorize(msg_ctx* c, const int32_t* d_lab, long long N, int depth, const uint8_t* d_pal,
@@ -700,6 +776,145 @@ int run_batch(msg_ctx* c, int n, F fn) {
       return rcs[w];
     }
     add(st[w]);
+  }
+  c->stats = tot;
+  return MSG_OK;
+}
+
+// Many floods per launch (msg_set_batch_floods): every frame of the call gets a workspace of its
+// own (a sub-context), phase 1 of each is queued on its stream with k_scan's small-batch loop off
+// (FloodRun multi), then ONE k_serial_multi launch pops all of them, one wave per flood.  A flood
+// that k_serial_multi leaves unfinished (mode 2: it handed back to batches after SERIAL_RUN clean
+// pops) is finished by the full engine, up to `inflight` at a time, speculative generations off.
+// frame(k, img, mk, H, W, lab, dst) describes frame k (device buffers; dst may be null).
+template <class F>
+int batch_many(msg_ctx* c, int n, int depth, const uint8_t* d_pal, F frame) {
+  if (n == 0) {
+    c->stats = msg_stats{};
+    return MSG_OK;
+  }
+  while ((int)c->msubs.size() < n) {
+    msg_ctx* sub = nullptr;
+    const int rc = msg_create(&sub, c->dev, 0);
+    if (rc) return fail(c, rc, "batch sub-context creation failed (%d)", rc);
+    c->msubs.push_back(sub);
+  }
+  if (c->wss_cap < n) {
+    dfree(c->d_wss);
+    c->wss_cap = 0;
+    HIPCHK(c, hipMalloc((void**)&c->d_wss, (size_t)n * sizeof(Ws)));
+    c->wss_cap = n;
+  }
+  std::vector<FloodRun> frs(n);
+  std::vector<Ws> h_ws(n);
+  std::vector<hipEvent_t> ev(n + 1, nullptr);
+  auto cleanup = [&]() {
+    for (auto e : ev)
+      if (e) (void)hipEventDestroy(e);
+  };
+  for (int k = 0; k <= n; ++k)
+    if (hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) {
+      cleanup();
+      return fail(c, MSG_EHIP, "hipEventCreate failed");
+    }
+  for (int k = 0; k < n; ++k) {
+    msg_ctx* x = c->msubs[k];
+    x->res_grid = c->res_grid;
+    x->fast = c->fast;
+    x->serk = false;
+    x->spec = false;  // the full engine finishes handed-back floods without the speculative engine
+    const uint8_t* img;
+    const int32_t* mk;
+    int H, W;
+    int32_t* lab;
+    uint8_t* dst;
+    frame(k, img, mk, H, W, lab, dst);
+    int rc = check_size(x, H, W, true);
+    if (!rc) rc = flood_begin(x, img, mk, H, W, x->own, frs[k], true);
+    if (!rc && hipEventRecord(ev[k], x->own) != hipSuccess) rc = fail(x, MSG_EHIP, "hipEventRecord failed");
+    if (rc) {
+      c->err = x->err;
+      for (int j = 0; j <= k; ++j) (void)hipStreamSynchronize(c->msubs[j]->own);
+      cleanup();
+      return rc;
+    }
+    h_ws[k] = frs[k].ws;
+  }
+  int rc = MSG_OK;
+  const int run_limit = c->many == 2 ? SERIAL_RUN : 0x7fffffff;
+  // the Ws array (copied before any launch reads it: hipMemcpyAsync from pageable memory returns
+  // once the source is consumed), then one wave per flood once every phase 1 is queued before it
+  if (hipMemcpyAsync(c->d_wss, h_ws.data(), (size_t)n * sizeof(Ws), hipMemcpyHostToDevice, c->own) != hipSuccess)
+    rc = fail(c, MSG_EHIP, "Ws upload failed");
+  for (int k = 0; k < n && !rc; ++k)
+    if (frs[k].N > 0 && hipStreamWaitEvent(c->own, ev[k], 0) != hipSuccess) rc = fail(c, MSG_EHIP, "stream wait failed");
+  if (!rc) {
+    LAUNCH(c, KID_SERIAL_MULTI, c->own, k_serial_multi, dim3(n), dim3(64), 0, c->d_wss, n, run_limit);
+    if (hipGetLastError() != hipSuccess || hipEventRecord(ev[n], c->own) != hipSuccess)
+      rc = fail(c, MSG_EHIP, "k_serial_multi launch failed");
+  }
+  for (int k = 0; k < n && !rc; ++k)
+    if (hipStreamWaitEvent(c->msubs[k]->own, ev[n], 0) != hipSuccess) rc = fail(c, MSG_EHIP, "stream wait failed");
+  if (rc) {
+    (void)hipStreamSynchronize(c->own);
+    for (int k = 0; k < n; ++k) (void)hipStreamSynchronize(c->msubs[k]->own);
+    cleanup();
+    return rc;
+  }
+  // every flood: the rest of its flood (a no-op loop of one group when k_serial_multi finished it)
+  // and its label map + colours, `inflight` host threads
+  const int K = std::max(1, std::min({c->inflight, n, MAX_INFLIGHT}));
+  std::vector<int> rcs(K, MSG_OK);
+  std::vector<msg_stats> st(K);
+  std::vector<std::thread> th;
+  for (int w = 0; w < K; ++w)
+    th.emplace_back([&, w]() {
+      if (hipSetDevice(c->dev) != hipSuccess) {
+        rcs[w] = MSG_EHIP;
+        return;
+      }
+      msg_stats acc{};
+      for (int k = w; k < n; k += K) {
+        msg_ctx* x = c->msubs[k];
+        const uint8_t* img;
+        const int32_t* mk;
+        int H, W;
+        int32_t* lab;
+        uint8_t* dst;
+        frame(k, img, mk, H, W, lab, dst);
+        int r = flood_loop(x, frs[k]);
+        if (!r) r = flood_end(x, frs[k], lab, depth, dst ? d_pal : nullptr, dst, nullptr);
+        if (r) {
+          rcs[w] = r;
+          return;
+        }
+        acc.batches += x->stats.batches;
+        acc.pops += x->stats.pops;
+        acc.host_syncs += x->stats.host_syncs;
+        acc.items += x->stats.items;
+        acc.pushes += x->stats.pushes;
+        acc.rows = x->stats.rows;
+        acc.cols = x->stats.cols;
+      }
+      st[w] = acc;
+    });
+  for (auto& t : th) t.join();
+  cleanup();
+  msg_stats tot{};
+  for (int w = 0; w < K; ++w) {
+    if (rcs[w]) {
+      c->err = "a flood of the batch failed";
+      for (int k = w; k < n; k += K)
+        if (!c->msubs[k]->err.empty()) c->err = c->msubs[k]->err;
+      return rcs[w];
+    }
+    tot.batches += st[w].batches;
+    tot.pops += st[w].pops;
+    tot.host_syncs += st[w].host_syncs;
+    tot.items += st[w].items;
+    tot.pushes += st[w].pushes;
+    tot.rows = st[w].rows;
+    tot.cols = st[w].cols;
   }
   c->stats = tot;
   return MSG_OK;
@@ -843,6 +1058,11 @@ extern "C" {
 
 int msg_abi_version(void) { return MSG_ABI_VERSION; }
 
+#ifndef MSEG_BUILD_ID
+#define MSEG_BUILD_ID "unknown"
+#endif
+const char* msg_build_id(void) { return MSEG_BUILD_ID; }
+
 int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
   if (!out || (flags & ~MSG_CREATE_HIGH_PRIORITY)) return MSG_EINVAL;
   *out = nullptr;
@@ -856,6 +1076,10 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
   // concurrent floods: the HIP runtime keeps streams of different priorities on different
   // hardware queues)
   int prio = 0;
+  if (hipSetDevice(c->dev) != hipSuccess) {  // the priority range below is the current device's
+    msg_destroy(c);
+    return MSG_EHIP;
+  }
   {
     const char* e = getenv("MSEG_STREAM_PRIORITY");
     int lo = 0, hi = 0;
@@ -905,6 +1129,10 @@ void msg_destroy(msg_ctx* c) {
   free_spec(c);
   for (msg_ctx* sub : c->subs) msg_destroy(sub);
   c->subs.clear();
+  for (msg_ctx* sub : c->msubs) msg_destroy(sub);
+  c->msubs.clear();
+  dfree(c->d_wss);
+  dfree(c->d_mstage);
   free_stage(c);
   dfree(c->d_pal);
   dfree(c->d_ctl);
@@ -1194,6 +1422,56 @@ int msg_watershed_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size
   if (!c || n < 0) return MSG_EINVAL;
   if (n > 0 && (!bgr || !bgr_stride || !markers || !marker_stride || !rows || !cols))
     return fail(c, MSG_EINVAL, "null batch array");
+  if (c->many && n > 0) {
+    // every frame staged (image, then its markers 16-B aligned), flooded in place together
+    std::vector<long long> off(n + 1, 0);
+    for (int k = 0; k < n; ++k) {
+      const int rc = host_args(c, bgr[k], bgr_stride[k], markers[k], marker_stride[k], rows[k], cols[k], true);
+      if (rc) return rc;
+      const long long N = (long long)rows[k] * cols[k];
+      off[k + 1] = off[k] + ((3 * N + 15) & ~15ll) + 4 * N;
+    }
+    HIPCHK(c, hipSetDevice(c->dev));
+    if (off[n] > c->mstage_cap) {
+      dfree(c->d_mstage);
+      c->mstage_cap = 0;
+      HIPCHK(c, hipMalloc((void**)&c->d_mstage, off[n] + 16));
+      c->mstage_cap = off[n];
+    }
+    auto img_of = [&](int k) { return c->d_mstage + off[k]; };
+    auto mk_of = [&](int k) {
+      return (int32_t*)(c->d_mstage + off[k] + ((3ll * rows[k] * cols[k] + 15) & ~15ll));
+    };
+    hipStream_t st = c->own;
+    for (int k = 0; k < n; ++k) {
+      if ((long long)rows[k] * cols[k] == 0) continue;
+      HIPCHK(c, hipMemcpy2DAsync(img_of(k), (size_t)cols[k] * 3, bgr[k], bgr_stride[k], (size_t)cols[k] * 3,
+                                 rows[k], hipMemcpyHostToDevice, st));
+      HIPCHK(c, hipMemcpy2DAsync(mk_of(k), (size_t)cols[k] * 4, markers[k], marker_stride[k],
+                                 (size_t)cols[k] * 4, rows[k], hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(c, hipStreamSynchronize(st));  // the floods run on the sub-contexts' streams
+    int rc = batch_many(c, n, 0, nullptr,
+                        [&](int k, const uint8_t*& img, const int32_t*& mk, int& H, int& W, int32_t*& lab, uint8_t*& dst) {
+                          img = img_of(k);
+                          mk = mk_of(k);
+                          H = rows[k];
+                          W = cols[k];
+                          lab = mk_of(k);
+                          dst = nullptr;
+                        });
+    if (rc) return rc;
+    for (int k = 0; k < n; ++k) {
+      if ((long long)rows[k] * cols[k] == 0) continue;
+      HIPCHK(c, hipMemcpy2DAsync(markers[k], marker_stride[k], mk_of(k), (size_t)cols[k] * 4, (size_t)cols[k] * 4,
+                                 rows[k], hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(c, hipStreamSynchronize(st));
+    for (int k = 0; k < n; ++k)
+      for (int j = 0; j < cols[k] && rows[k] > 0; ++j)
+        if (markers[k][j] != WSHED) return fail(c, MSG_ESTATE, "label read-back of frame %d failed the frame-border check", k);
+    return MSG_OK;
+  }
   return run_batch(c, n, [&](int k, msg_ctx* x) {
     return msg_watershed(x, bgr[k], bgr_stride[k], markers[k], marker_stride[k], rows[k], cols[k]);
   });
@@ -1228,10 +1506,32 @@ int msg_watershed_colorize_batch_dev(msg_ctx* c, int n, const void* const* d_bgr
   HIPCHK(c, hipSetDevice(c->dev));
   // the inputs may still be in flight on the caller's stream: the floods run on other streams
   HIPCHK(c, stream ? hipStreamSynchronize((hipStream_t)stream) : hipDeviceSynchronize());
+  if (c->many) {
+    for (int k = 0; k < n; ++k) {
+      if (rows[k] < 0 || cols[k] < 0) return fail(c, MSG_EINVAL, "negative size of frame %d", k);
+      if ((long long)rows[k] * cols[k] > 0 && (!d_bgr[k] || !d_markers_in[k] || !d_labels[k]))
+        return fail(c, MSG_EINVAL, "null device pointer of frame %d", k);
+    }
+    return batch_many(c, n, depth, (const uint8_t*)d_palette_bgr,
+                      [&](int k, const uint8_t*& img, const int32_t*& mk, int& H, int& W, int32_t*& lab, uint8_t*& dst) {
+                        img = (const uint8_t*)d_bgr[k];
+                        mk = (const int32_t*)d_markers_in[k];
+                        H = rows[k];
+                        W = cols[k];
+                        lab = (int32_t*)d_labels[k];
+                        dst = (uint8_t*)d_dst_bgr[k];
+                      });
+  }
   return run_batch(c, n, [&](int k, msg_ctx* x) {
     return msg_watershed_colorize_dev(x, d_bgr[k], d_markers_in[k], d_labels[k], rows[k], cols[k],
                                       depth, d_palette_bgr, d_dst_bgr[k], nullptr, nullptr);
   });
+}
+
+int msg_set_batch_floods(msg_ctx* c, int mode) {
+  if (!c || mode < 0 || mode > 2) return MSG_EINVAL;
+  c->many = mode;
+  return MSG_OK;
 }
 
 int msg_gray_hist_dev(msg_ctx* c, const void* d_bgr, int rows, int cols, void* d_gray,

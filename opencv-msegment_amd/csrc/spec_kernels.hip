@@ -26,10 +26,12 @@
 //     pop sequence of the generation.  Flattened into "virtual items" (one per pop, with its
 //     deferred pushes) they go through the batch engine's own ordered append (k_scan,
 //     k_scatter), which keeps every bucket in exact serial FIFO order;
-//   * an execution that overflows its lane's queue (SPEC_QCAP live entries) or scratch
-//     (SPEC_RL records) while all its inputs are final ends the regime: the prefix before it is
-//     committed and the batch engine pops that item and its cascade (serial pops), after which
-//     the regime resumes (SpecCtl.block).
+//   * a lane's cascade queue keeps its SPEC_QCAP smallest keys in LDS and spills the rest to a
+//     chunk of the round's pool (cold keys, each larger than every LDS key); records past SPEC_RL
+//     go to pool chunks too.  Only an execution beyond those chunks (SPEC_CCAP live entries,
+//     SPEC_RL + SPEC_NX * SPEC_XCH records) while all its inputs are final ends the regime: the
+//     prefix before it is committed and the batch engine pops that item and its cascade (serial
+//     pops), after which the regime resumes (SpecCtl.block).
 // scripts/exp/spec_rounds.c is the CPU prototype of exactly this scheme (bit-exact against the
 // oracle on mosaic+noise, random and album frames; it also counts the rounds).
 #include <hip/hip_runtime.h>
@@ -40,6 +42,14 @@
 namespace msg {
 
 constexpr unsigned SPEC_RMAX = (1u << 22) - 1;
+#ifndef MSEG_SPEC_MINB
+#define MSEG_SPEC_MINB 2  // two blocks per CU (the LDS allows two): caps the registers at 256
+#endif
+#ifndef MSEG_SPEC_RFW
+#define MSEG_SPEC_RFW 2
+#endif
+constexpr int SPEC_RFW = MSEG_SPEC_RFW;  // cold keys loaded together in a refill pass
+static_assert(SPEC_NX == 4, "k_spec_round keeps SPEC_NX record chunk bases in four registers");
 
 __device__ __forceinline__ unsigned long long spec_claim(unsigned tag, int rank, unsigned popped) {
   return ((unsigned long long)tag << 32) | ((unsigned long long)(SPEC_RMAX - (unsigned)rank) << 1) | popped;
@@ -74,6 +84,15 @@ __device__ __forceinline__ unsigned long long srec_pack(int p, int lab, unsigned
 __device__ __forceinline__ unsigned long long smix(unsigned long long h, unsigned long long v) {
   h ^= v + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
   return h * 0xff51afd7ed558ccdull;
+}
+
+// Record k of an execution: lane scratch, then the pool chunks xb0..xb3 (SPEC_XCH records each).
+__device__ __forceinline__ unsigned long long* spec_rec_at(unsigned long long* tmp, unsigned long long* sxp, int k,
+                                                           int xb0, int xb1, int xb2, int xb3) {
+  if (k < SPEC_RL) return tmp + k;
+  const int c = (k - SPEC_RL) / SPEC_XCH, o = (k - SPEC_RL) % SPEC_XCH;
+  const int xb = c == 0 ? xb0 : c == 1 ? xb1 : c == 2 ? xb2 : xb3;
+  return sxp + (size_t)xb + o;
 }
 
 struct SpecView {
@@ -195,13 +214,14 @@ __device__ void spec_finalize(Ctl* ctl, int P, int n, unsigned T, unsigned G, un
     ctl->sdeal.v = P;
     ctl->sfc.v = NONE;
     ctl->sovf.v = NONE;
+    ctl->sxtop.v = 0;  // every execution of this round has copied its records to the log
   }
   s.ticket = 0;
 }
 
 // One round.  Waves take 64 consecutive ranks at a time from [Pold, n) in dispatch order:
 // [Pold, P) promote their claims, [P, n) execute.
-__global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
+__global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
   Ctl* ctl = ws.ctl;
   if (ctl->bat.mode != 3 || ctl->spec.state != 1 || ctl->error) return;
   __shared__ unsigned long long lq[SPEC_QCAP * SPEC_BS];  // per-lane cascade queues, [entry][lane]
@@ -397,6 +417,8 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
     unsigned long long sig = 0;
     int nrec = 0;
     int rbase = -1;  // >= 0: the cascade was replayed from the previous round's log records here
+    int xb0 = -1, xb1 = -1, xb2 = -1, xb3 = -1;  // record chunks past SPEC_RL (SPEC_NX = 4)
+#define rec_at(k) spec_rec_at(tmp, ws.sxp, (k), xb0, xb1, xb2, xb3)
     if (ex) {
       // ---- the top pop, then the cascade (levels < L, lowest first, FIFO) ----
       // Every pop's writes (claims, label, record) are issued AFTER the loads of the next pop's
@@ -404,7 +426,109 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
       // stores waits for their acknowledgements too.  The next pop therefore sees its
       // predecessor's writes through a patch (that pop's pixel and pushes) instead of memory;
       // everything older was issued before its loads.
-      int nq = 0;
+      // The lane's cascade queue: keys {level, push sequence, pixel} (the serial order of a
+      // cascade is the key order: lowest level first, FIFO within a level).  The SPEC_QCAP
+      // smallest live keys are "hot" in LDS; the rest are "cold" in a chunk of the round's pool,
+      // every cold key larger than every hot one.
+      int nq = 0, nc = 0;   // hot / cold keys
+      int cb = -1;          // cold chunk in ws.sxp
+      unsigned cmin = 256;  // lowest level among the cold keys
+      unsigned qseq = 0;    // pushes of this execution
+      auto pool_get = [&](int sz) -> int {
+        const int b = atomicAdd(&ctl->sxtop.v, sz);
+        return ((long long)b + sz <= ws.sxcap) ? b : -1;
+      };
+      auto cold_add = [&](unsigned long long k) {
+#ifdef MSEG_SPEC_NOSPILL
+        ovf = cap = true;
+        return;
+#endif
+        if (cb < 0 && (cb = pool_get(SPEC_CCAP)) < 0) {
+          ovf = cap = true;
+          return;
+        }
+        if (nc >= SPEC_CCAP) {
+          ovf = cap = true;
+          return;
+        }
+        ws.sxp[(size_t)cb + nc++] = k;
+        cmin = min(cmin, (unsigned)(k >> 52));
+      };
+      auto qpush = [&](unsigned t, int pix) {
+        const unsigned long long k =
+            ((unsigned long long)t << 52) | ((unsigned long long)(qseq++ & 0xffffffu) << 28) | (unsigned)pix;
+        if (nc > 0 && t >= cmin) {  // above the smallest cold key: cold too
+          cold_add(k);
+          return;
+        }
+        if (nq < SPEC_QCAP) {
+          lq[(nq++) * SPEC_BS + tid] = k;
+          return;
+        }
+        int mi = 0;  // hot is full: the larger of k and the largest hot key goes cold
+        unsigned long long mk = lq[tid];
+        for (int e = 1; e < SPEC_QCAP; ++e) {
+          const unsigned long long v = lq[e * SPEC_BS + tid];
+          if (v > mk) {
+            mk = v;
+            mi = e;
+          }
+        }
+        if (k > mk) {
+          cold_add(k);
+        } else {
+          cold_add(mk);
+          lq[mi * SPEC_BS + tid] = k;
+        }
+      };
+      // hot empty, cold not: the SPEC_QCAP smallest cold keys become hot (one pass keeping the
+      // smallest seen, one pass compacting the rest in place)
+      auto refill = [&]() {
+        const size_t b = (size_t)cb;
+        unsigned long long hmax = 0;
+        int hmi = 0;
+        for (int k0 = 0; k0 < nc; k0 += SPEC_RFW) {
+          unsigned long long v[SPEC_RFW];
+  #pragma unroll
+          for (int k = 0; k < SPEC_RFW; ++k) v[k] = (k0 + k < nc) ? ws.sxp[b + k0 + k] : 0ull;
+  #pragma unroll
+          for (int k = 0; k < SPEC_RFW; ++k) {
+            if (k0 + k >= nc) continue;
+            if (nq < SPEC_QCAP) {
+              lq[nq * SPEC_BS + tid] = v[k];
+              if (v[k] > hmax) {
+                hmax = v[k];
+                hmi = nq;
+              }
+              ++nq;
+            } else if (v[k] < hmax) {
+              lq[hmi * SPEC_BS + tid] = v[k];
+              hmax = 0;
+              for (int e = 0; e < SPEC_QCAP; ++e) {
+                const unsigned long long u = lq[e * SPEC_BS + tid];
+                if (u > hmax) {
+                  hmax = u;
+                  hmi = e;
+                }
+              }
+            }
+          }
+        }
+        int w = 0;
+        cmin = 256;
+        for (int k0 = 0; k0 < nc; k0 += SPEC_RFW) {
+          unsigned long long v[SPEC_RFW];
+  #pragma unroll
+          for (int k = 0; k < SPEC_RFW; ++k) v[k] = (k0 + k < nc) ? ws.sxp[b + k0 + k] : 0ull;
+  #pragma unroll
+          for (int k = 0; k < SPEC_RFW; ++k) {
+            if (k0 + k >= nc || v[k] <= hmax) continue;
+            ws.sxp[b + w++] = v[k];
+            cmin = min(cmin, (unsigned)(v[k] >> 52));
+          }
+        }
+        nc = w;
+      };
       unsigned dm = 0, ppm = 0;  // deferred pushes; the pending pop's pushes (all levels)
       if (mylab != WSHED) {
   #pragma unroll
@@ -412,12 +536,8 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
           if (!((pm >> d) & 1u)) continue;
           ppm |= 1u << d;
           const unsigned t = (wp >> (8 * d)) & 255u;
-          if ((int)t < L) {
-            if (nq < SPEC_QCAP) lq[(nq++) * SPEC_BS + tid] = ((unsigned long long)t << 32) | (unsigned)nbp[d];
-            else ovf = cap = true;
-          } else {
-            dm |= 1u << d;
-          }
+          if ((int)t < L) qpush(t, nbp[d]);
+          else dm |= 1u << d;
         }
       }
       unsigned long long rec = srec_pack(p, mylab, dm);
@@ -432,7 +552,7 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
   #pragma unroll
         for (int d = 0; d < 4; ++d)
           if ((ppm >> d) & 1u) claim_max(&spx[pz[d]].cl[par], spec_claim(T, j, 0u));
-        tmp[k] = rec;
+        *rec_at(k) = rec;
       };
       if (nq > 0 && !ovf && !gchg && j < ovlim) {
         const int4 pr = ws.srec[(size_t)ppar * SPEC_WIN + j];
@@ -452,25 +572,26 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
           }
           nrec = pr.y;
           rbase = pr.x;
-          nq = 0;
+          nq = nc = 0;
           ppm = 0;
           py = -1;
         }
       }
-      // next pop: the oldest entry of the lowest level in the lane's LDS queue
+      // next pop: the smallest key (lowest level, oldest push) of the lane's queue
       auto select = [&]() -> int {
+        if (nq == 0) refill();
         int bi = 0;
         unsigned long long be = lq[tid];
         for (int k = 1; k < nq; ++k) {
           const unsigned long long e = lq[k * SPEC_BS + tid];
-          if ((e >> 32) < (be >> 32)) {
+          if (e < be) {
             be = e;
             bi = k;
           }
         }
-        for (int k = bi; k + 1 < nq; ++k) lq[k * SPEC_BS + tid] = lq[(k + 1) * SPEC_BS + tid];
         --nq;
-        return (int)(uint32_t)be;
+        lq[bi * SPEC_BS + tid] = lq[nq * SPEC_BS + tid];
+        return (int)(be & 0x0fffffffull);
       };
       int y = 0;
       unsigned wy = 0;
@@ -486,16 +607,28 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
         r2 = spec_load(ws, V, nby[2]);
         r3 = spec_load(ws, V, nby[3]);
       };
-      bool more = nq > 0 && !ovf;
+      bool more = nq + nc > 0 && !ovf;
       if (more) {
         y = select();
         issue_loads();
       }
       if (py >= 0) issue_writes(0);
       while (more) {
-        if (nrec >= SPEC_RL) {
-          ovf = cap = true;
-          break;
+        if (nrec >= SPEC_RL && (nrec - SPEC_RL) % SPEC_XCH == 0) {  // the next record starts a chunk
+          const int c = (nrec - SPEC_RL) / SPEC_XCH;
+#ifdef MSEG_SPEC_NOSPILL
+          const int b = -1;
+#else
+          const int b = c < SPEC_NX ? pool_get(SPEC_XCH) : -1;
+#endif
+          if (b < 0) {
+            ovf = cap = true;
+            break;
+          }
+          if (c == 0) xb0 = b;
+          else if (c == 1) xb1 = b;
+          else if (c == 2) xb2 = b;
+          else xb3 = b;
         }
 #ifdef MSEG_SPEC_PROF
         const long long q1 = (long long)__builtin_amdgcn_s_memtime();
@@ -533,12 +666,8 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
             if (v[d] != 0) continue;
             pmy |= 1u << d;
             const unsigned t = (wy >> (8 * d)) & 255u;
-            if ((int)t < L) {
-              if (nq < SPEC_QCAP) lq[(nq++) * SPEC_BS + tid] = ((unsigned long long)t << 32) | (unsigned)nby[d];
-              else ovf = cap = true;
-            } else {
-              dmy |= 1u << d;
-            }
+            if ((int)t < L) qpush(t, nby[d]);
+            else dmy |= 1u << d;
           }
         }
         rec = srec_pack(y, lab, dmy);
@@ -549,7 +678,7 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
   #pragma unroll
         for (int d = 0; d < 4; ++d) pz[d] = nby[d];
         const int k = nrec++;
-        more = nq > 0 && !ovf;
+        more = nq + nc > 0 && !ovf;
 #ifdef MSEG_SPEC_PROF
         const long long q3 = (long long)__builtin_amdgcn_s_memtime();
 #endif
@@ -585,7 +714,7 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
       if (!ovf && rbase < 0) {
         if ((long long)base + nrec > ws.slogcap) ovf = cap = true;  // generation log full
         else
-          for (int k = 0; k < nrec; ++k) ws.slog[base + k] = tmp[k];
+          for (int k = 0; k < nrec; ++k) ws.slog[base + k] = *rec_at(k);
       }
       sig = smix(sig, ((unsigned long long)nrec << 1) | (ovf ? 1ull : 0ull));
       ws.srec[(size_t)par * SPEC_WIN + j] = make_int4(base, ovf ? 0 : nrec, (int)T, cap ? 1 : 0);
@@ -607,7 +736,7 @@ __global__ __launch_bounds__(SPEC_BS) void k_spec_round(Ws ws) {
             if ((dmy >> d) & 1u) dn[nbi(y + marg, d, Wt) - marg] = T;
         };
         if (rbase < 0)
-          for (int k = 0; k < nrec; ++k) mark(tmp[k]);
+          for (int k = 0; k < nrec; ++k) mark(*rec_at(k));
         const int4 pr = ws.srec[(size_t)ppar * SPEC_WIN + j];
         if (V.hasprev && pr.z == (int)(T - 1u))
           for (int k = 0; k < pr.y; ++k) mark(ws.slog[pr.x + k]);

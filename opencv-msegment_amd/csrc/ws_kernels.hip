@@ -831,6 +831,7 @@ __device__ void spec_begin(Ctl* ctl, Batch& nb, int L, int bstart, int navail) {
   ctl->sdeal.v = 0;
   s.ticket = 0;
   ctl->slogtop.v = 0;
+  ctl->sxtop.v = 0;
   s.fallback = 0;
   s.ftile = 0;
   s.tgen = (long long)__builtin_amdgcn_s_memrealtime();
@@ -1457,7 +1458,7 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
   } else if (cb.nchunk > 0) {
     return;  // k_scatter commits it
   }
-  small_loop(ws);
+  if (!ws.multi) small_loop(ws);  // a many-floods batch pops in k_serial_multi instead
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1541,7 +1542,10 @@ __device__ Batch scan_body(const Ws& ws) {
   if (tid < NQ) {  // pushes appended: one atomic per wave of levels (no block barrier)
     int dp = s_tail[tid] - oldt;
     dp = wave_sum(dp);
-    if ((tid & 63) == 0 && dp) atomicAdd((unsigned long long*)&ctl->pushes, (unsigned long long)dp);
+    if ((tid & 63) == 0 && dp) {
+      atomicAdd((unsigned long long*)&ctl->pushes, (unsigned long long)dp);
+      atomicAdd((unsigned long long*)&ctl->spushes, (unsigned long long)dp);
+    }
   }
   if (B.mode == 0 && tid < B.nseg) {  // advance every segment's bucket head by what it committed
     const Seg s = s_seg[tid];
@@ -1552,6 +1556,7 @@ __device__ Batch scan_body(const Ws& ws) {
       ctl->pops += ncommit;
       ctl->items += B.n;
     }
+    ctl->spops += ncommit;
     Batch cb = B;
     cb.ncommit = ncommit;
     cb.nchunk = nch;
@@ -1976,7 +1981,10 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
       atomicAdd(&s_head[r_sg.L], max(0, min(ncommit - r_sg.rank, r_sg.n)));
     if (tid < NQ) {
       dp = wave_sum(dp);
-      if ((tid & 63) == 0 && dp) atomicAdd((unsigned long long*)&ctl->pushes, (unsigned long long)dp);
+      if ((tid & 63) == 0 && dp) {
+        atomicAdd((unsigned long long*)&ctl->pushes, (unsigned long long)dp);
+        atomicAdd((unsigned long long*)&ctl->fpushes, (unsigned long long)dp);
+      }
     }
     __syncthreads();
     form_batch(qb, s_head, s_tail, s_minpush, s_wcap, nsegs, &s_nseg, &s_n);
@@ -2026,6 +2034,7 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
     }
     if (tid == 0) {
       ctl->pops += ncommit;
+      ctl->fpops += ncommit;
       ctl->items += B.n;
       Batch nb;
       nb.mode = 0;
@@ -2801,7 +2810,8 @@ __device__ __forceinline__ void ser_flush(const Ws& ws, int* mkb, int* dummy, Se
 // interrupt (batches pay again), at the speculative engine's hand-back points, or on an error.
 // Bucket records and rings in LDS are written by lane 0 (LDS is in order within the wave).
 __device__ __forceinline__ void ser_run(const Ws& ws, int4* s_bk, int (*s_bring)[SER_RING], unsigned long long* ne,
-                                        int& err, SerStat& S, int spec_block, long long cool_lim) {
+                                        int& err, SerStat& S, int spec_block, long long cool_lim,
+                                        int run_limit = SERIAL_RUN) {
   const int lane = lane_id();
   const int Wt = ws.Wt, marg = ws.marg;
   int* const mkb = ws.mk - marg;
@@ -2816,7 +2826,7 @@ __device__ __forceinline__ void ser_run(const Ws& ws, int4* s_bk, int (*s_bring)
     const unsigned long long t0 = ser_clock();
     const int lo = ne0 ? __builtin_ctzll(ne0) : ne1 ? 64 + __builtin_ctzll(ne1)
                  : ne2 ? 128 + __builtin_ctzll(ne2) : ne3 ? 192 + __builtin_ctzll(ne3) : NQ;
-    if (lo >= NQ || run >= SERIAL_RUN) break;
+    if (lo >= NQ || run >= run_limit) break;
     if (spec_block > 0 && lo >= spec_block) break;  // the cascade that stopped the speculative engine is done
     if (S.pops >= cool_lim) break;                  // its cooldown is over
     if (ws.spec_lazy && S.pops >= 4096) break;      // the engine is being allocated: let it take over
@@ -3043,6 +3053,91 @@ __global__ __launch_bounds__(64) void k_serial(Ws ws, int iter) {
     __hip_atomic_store(ws.hmir + 6, fast_batch(nb, ctl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 7, nb.mode == 4 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_serial_multi: the serial pops of MANY floods in one launch (the batch entry points' many-floods
+// mode, msg_set_batch_floods): block f = one wave = flood f, each flood in its own workspace
+// (wss[f]).  Photographs and scattered seeds put cv::watershed's exact order in its serial regime
+// -- chains of dependent pops, a lone wave's memory latency per pop -- so a
+// batch of such frames is bound by the number of floods in flight: here every flood of the call
+// (hundreds), instead of the 4-8 streams over which the full engine's floods overlap.  Each wave
+// runs k_serial's pop loop (ser_run) on its flood from wherever it stands (after phase 1, or after
+// a batch of the full engine) until its queue is empty, or until run_limit consecutive pops pushed
+// nothing below their own level (batches pay again: the host finishes that flood with the full
+// engine), then writes the queue state back and forms the next batch as k_serial does.  No wave
+// waits for another: each block only touches its own flood.
+__global__ __launch_bounds__(64) void k_serial_multi(const Ws* __restrict__ wss, int n, int run_limit) {
+  const int f = blockIdx.x;
+  if (f >= n) return;
+  const Ws ws = wss[f];
+  Ctl* ctl = ws.ctl;
+  __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ];
+  __shared__ int s_bring[NQ][SER_RING];
+  __shared__ Seg s_seg[NQ];
+  __shared__ int s_nseg, s_n;
+  __shared__ int4 s_bk[NQ];
+  __shared__ unsigned long long s_ne[4];
+  const int lane = lane_id();
+  const Batch B0 = ctl->bat;
+  if (ctl->done || ctl->error || B0.n == 0 || (B0.mode != 0 && B0.mode != 4)) return;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int b = 64 * k + lane;
+    const int hd = ctl->qhead[b], tl = ctl->qtail[b];
+    s_qbase[b] = ctl->qbase[b];
+    s_bk[b] = make_int4(hd, tl, s_qbase[b], tl);
+    const unsigned long long m = __ballot(tl > hd);
+    if (lane == 0) s_ne[k] = m;
+  }
+  wave_sync();
+  SerStat S;
+  int err = 0;
+  ser_run(ws, s_bk, s_bring, s_ne, err, S, 0, 1ll << 62, run_limit);
+  wave_sync();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int4 r = s_bk[64 * k + lane];
+    s_head[64 * k + lane] = r.x;
+    s_tail[64 * k + lane] = r.y;
+  }
+  wave_sync();
+  form_batch(s_qbase, s_head, s_tail, 0, 0, s_seg, &s_nseg, &s_n);
+  wave_sync();
+  const int ns = s_nseg;
+  for (int k = lane; k < NQ; k += 64) {
+    ctl->qhead[k] = s_head[k];
+    ctl->qtail[k] = s_tail[k];
+  }
+  for (int k = lane; k < ns; k += 64) ctl->seg[k] = s_seg[k];
+  int q = 0;
+#pragma unroll
+  for (int k = 0; k < NQ / 64; ++k) q += s_tail[lane + 64 * k] - s_head[lane + 64 * k];
+  q = wave_sum(q);
+  if (lane == 0) {
+    Batch nb;
+    nb.mode = 0;
+    nb.epoch = B0.epoch + 1;
+    nb.ncommit = 0;
+    nb.nchunk = 0;
+    nb.rrun = 0;
+    nb.nseg = ns;
+    nb.n = (ns > 0) ? s_n : 0;
+    nb.L = (ns > 0) ? s_seg[0].L : -1;
+    nb.bstart = (ns > 0) ? s_seg[0].bstart : 0;
+    ctl->bat = nb;
+    ctl->wcap = 0;
+    ctl->cut = NONE;
+    ctl->segcut = NONE;
+    ctl->minpush = NQ;
+    ctl->remaining = q;
+    ctl->batches += S.pops;
+    ctl->pops += S.pops;
+    ctl->items += S.pops;
+    ctl->pushes += S.pushes;
+    if (err) ctl->error |= err;
+    if (nb.n == 0 && !err) ctl->done = 1;
   }
 }
 

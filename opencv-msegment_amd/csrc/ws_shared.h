@@ -76,8 +76,11 @@ constexpr int SPEC_BS = 256;        // threads per k_spec_round block
 #ifndef MSEG_SPEC_RL
 #define MSEG_SPEC_RL 256
 #endif
-constexpr int SPEC_QCAP = MSEG_SPEC_QCAP;  // per-lane cascade queue (LDS): more live entries = overflow
-constexpr int SPEC_RL = MSEG_SPEC_RL;      // records per execution (lane scratch): more = overflow
+constexpr int SPEC_QCAP = MSEG_SPEC_QCAP;  // per-lane cascade queue in LDS ("hot": the smallest keys)
+constexpr int SPEC_RL = MSEG_SPEC_RL;      // records per execution in lane scratch, the rest in pool chunks
+constexpr int SPEC_CCAP = 4096;     // "cold" cascade entries of one execution (a pool chunk): more = overflow
+constexpr int SPEC_XCH = 2048;      // records per pool chunk past the first SPEC_RL
+constexpr int SPEC_NX = 4;          // such chunks per execution: more records = overflow
 constexpr int SPEC_ROUNDS_MAX = 64; // rounds per generation before the stable prefix is committed
 constexpr int SPEC_FT = 1024;       // items per k_spec_flatten tile
 constexpr int SPEC_QUIET = 4096;    // a generation this large without a cascade ends the regime
@@ -175,6 +178,8 @@ struct Ctl {
   long long pops;
   long long items;   // sum of batch sizes resolved (committed or not)
   long long pushes;  // committed pushes appended to buckets
+  long long fpops, fpushes;  // of which committed by k_commit_fast (the roofline's bytes per launch)
+  long long spops, spushes;  // of which committed by k_scan + k_scatter (batches above SMALL_MAX)
   unsigned rsv;      // epoch of the last batch k_resolve (or k_spec_flatten) decided
   int pad;
   SpecCtl spec;
@@ -192,6 +197,7 @@ struct Ctl {
   Hot sdeal;     // dispatch-order rank dealing
   Hot sfc, sovf; // lowest changed / overflowing rank of this round
   Hot slogtop;   // generation log records used
+  Hot sxtop;     // k_spec_round's chunk pool used this round (cold cascade queues, record chunks)
 };
 
 static_assert(__builtin_offsetof(Ctl, error) % 8 == 0 && __builtin_offsetof(Ctl, rgive) == __builtin_offsetof(Ctl, error) + 4,
@@ -229,10 +235,15 @@ struct Ws {
   unsigned long long* sflag; // k_spec_flatten tile prefixes {generation tag, inclusive sum}
   unsigned* sdirt;           // 2 x snp change marks per round parity: round tag of the last changed
                              // execution whose claims (old or new) covered the pixel
+  unsigned long long* sxp;   // chunk pool of a round: an execution's cold cascade queue (SPEC_CCAP
+                             // keys) and its records past SPEC_RL (SPEC_XCH each), reset every round
+  long long sxcap;
   long long snp;
   long long slogcap;
   int spec_lazy;     // 1: engine enabled, workspace not allocated yet (k_scan reports spec_want)
   int serk;          // 1: the serial-pop regime runs in k_serial (mode 4), 0: inside k_scan
+  int multi;         // 1: a flood of a many-floods batch: k_scan stops after each commit (no
+                     // small-batch loop), k_serial_multi pops it together with the others
   int H, W;
   int Wt;            // tiles per tile row = ceil(W / 4)
   int marg;          // tiled entries of margin before mk / w4 (mk - marg starts the state array)

@@ -215,6 +215,11 @@ class Segmenter:
         """Floods kept in flight by the batch calls (1..8; 1 = back to back)."""
         self._check(self._L.msg_set_batch_inflight(self._h, int(k)))
 
+    def set_batch_floods(self, mode=1):
+        """Many floods per launch in the batch calls (msegment.h msg_set_batch_floods): 0 off, 1 every
+        flood serial to its end in one kernel (one wave per flood), 2 plateaus handed to batches."""
+        self._check(self._L.msg_set_batch_floods(self._h, int(mode)))
+
     def set_resolve_grid(self, blocks=0):
         """Blocks per k_resolve launch (0 = the default); a performance knob only."""
         self._check(self._L.msg_set_resolve_grid(self._h, int(blocks)))

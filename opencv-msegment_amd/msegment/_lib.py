@@ -5,6 +5,7 @@ point raises.  The CPU restatement under oracle/ is test infrastructure and is n
 here.
 """
 import ctypes
+import hashlib
 import os
 import subprocess
 
@@ -33,12 +34,12 @@ def MSG_NC_MASK(k):
 
 # every symbol include/msegment.h declares (checked by tests/test_abi.py)
 EXPORTS = (
-    "msg_create", "msg_destroy", "msg_last_error", "msg_abi_version", "msg_get_stats",
+    "msg_create", "msg_destroy", "msg_last_error", "msg_abi_version", "msg_build_id", "msg_get_stats",
     "msg_watershed", "msg_colorize", "msg_watershed_colorize", "msg_watershed_batch",
     "msg_watershed_dev", "msg_colorize_dev", "msg_watershed_colorize_dev", "msg_edge_weights_dev",
     "msg_set_profiling", "msg_get_kernel_profile", "msg_set_diag", "msg_set_speculative",
     "msg_set_fast_commit", "msg_set_serial_kernel",
-    "msg_set_batch_inflight", "msg_set_resolve_grid", "msg_watershed_colorize_batch_dev",
+    "msg_set_batch_inflight", "msg_set_batch_floods", "msg_set_resolve_grid", "msg_watershed_colorize_batch_dev",
     "msg_gray_hist_dev", "msg_nc_levels", "msg_nc_marker_lut", "msg_nc_markers_dev",
     "msg_nc_marker_stage_dev", "msg_nc_marker_stage",
     "msg_blur_mask_size", "msg_shape_markers_dev", "msg_shape_markers",
@@ -63,7 +64,9 @@ class Stats(ctypes.Structure):
                 ("spec_executions", ctypes.c_int64), ("spec_cascade_pops", ctypes.c_int64),
                 ("spec_fallbacks", ctypes.c_int64), ("spec_replays", ctypes.c_int64),
                 ("spec_cooldowns", ctypes.c_int64), ("spec_gen_pops", ctypes.c_int64),
-                ("spec_gen_us", ctypes.c_int64)]
+                ("spec_gen_us", ctypes.c_int64),
+                ("fast_pops", ctypes.c_int64), ("fast_pushes", ctypes.c_int64),
+                ("scatter_pops", ctypes.c_int64), ("scatter_pushes", ctypes.c_int64)]
 
 
 class KernelProfile(ctypes.Structure):
@@ -76,12 +79,25 @@ class BrightLevel(ctypes.Structure):
     _fields_ = [("start", ctypes.c_int32), ("end", ctypes.c_int32), ("count", ctypes.c_int32)]
 
 
-NKERNELS = 24  # MSG_NKERNELS (include/msegment.h; tests/test_abi.py checks the two agree)
+NKERNELS = 25  # MSG_NKERNELS (include/msegment.h; tests/test_abi.py checks the two agree)
 
 
 def build(arch="gfx950"):
     """Compile libmsegment.so in-tree with hipcc (no GPU needed)."""
     subprocess.check_call(["make", "-s", "-C", CSRC, "ARCH=%s" % arch])
+
+
+def source_id(csrc=CSRC):
+    """The id libmsegment.so carries (msg_build_id): SHA-256 prefix of csrc's sources (sorted by
+    name) followed by include/msegment.h -- the same bytes the Makefile's BUILD_ID hashes."""
+    names = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h", ".cpp")))
+    paths = [os.path.join(csrc, f) for f in names]
+    paths.append(os.path.join(os.path.dirname(os.path.dirname(csrc)), "include", "msegment.h"))
+    h = hashlib.sha256()
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 _lib = None
@@ -102,6 +118,16 @@ def load():
     except ImportError:
         pass
     L = ctypes.CDLL(LIB_PATH)
+    if not os.environ.get("MSEGMENT_LIB") and os.path.isdir(CSRC):
+        L.msg_build_id.argtypes = []
+        L.msg_build_id.restype = ctypes.c_char_p
+        # the in-tree library must be built from the sources next to it: a stale .so (shipped to a
+        # box that did not rebuild) would silently run old kernels.  MSEGMENT_LIB (A/B builds of
+        # other variants) is taken as given.
+        built, want = L.msg_build_id().decode(), source_id()
+        if built != want:
+            raise ImportError("libmsegment.so is stale: built from sources %s, csrc/ is %s "
+                              "(run __graft_entry__.build())" % (built, want))
     vp = ctypes.c_void_p
     sz = ctypes.c_size_t
     i = ctypes.c_int
@@ -145,6 +171,9 @@ def load():
     L.msg_get_kernel_profile.restype = i
     L.msg_set_batch_inflight.argtypes = [vp, i]
     L.msg_set_batch_inflight.restype = i
+    if hasattr(L, "msg_set_batch_floods"):  # (MSEGMENT_LIB A/B builds of earlier rounds lack it)
+        L.msg_set_batch_floods.argtypes = [vp, i]
+        L.msg_set_batch_floods.restype = i
     L.msg_set_resolve_grid.argtypes = [vp, i]
     L.msg_set_resolve_grid.restype = i
     L.msg_watershed_colorize_batch_dev.argtypes = [vp, i, vp, vp, vp, vp, vp, i, vp, vp, vp]

@@ -37,7 +37,7 @@ def nc_option_flags(options, filter_mask_size):
     are valid in OpenCV but do not fit the option bits (MsegError, never a silent wrap).
     BILATERIAL: every size <= 0 behaves as 0 in bilateralFilter (sigma <= 0 -> 1, radius
     cvRound(1.5)), so it is passed as 0; sizes above 255 do not fit the option bits (MsegError).
-    MSegmentNative.ncMaskBits is the same rule on the Java side."""
+    MSegmentNative.ncFilterBits is the same rule on the Java side."""
     from . import MsegError, _lib
 
     opts = set(options)

@@ -26,7 +26,28 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_binding_load():
     L = _lib.load()
-    assert L.msg_abi_version() == 4
+    assert L.msg_abi_version() == 5
+
+
+def test_build_id_matches_sources():
+    """libmsegment.so is built from the csrc/ next to it (msg_build_id = the Makefile's BUILD_ID);
+    _lib.load() refuses a stale library."""
+    L = _lib.load()
+    assert L.msg_build_id().decode() == _lib.source_id()
+
+
+def test_stats_struct_matches_header():
+    """The ctypes Stats mirror has exactly the header's msg_stats fields (all int64): a smaller
+    caller struct would be overrun by msg_get_stats."""
+    hdr = open(os.path.join(ROOT, "include", "msegment.h")).read()
+    body = re.search(r"typedef struct msg_stats \{(.*?)\} msg_stats;", hdr, flags=re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    n = 0
+    for decl in re.findall(r"int64_t\s+([^;]+);", body):
+        for name in decl.split(","):
+            m = re.match(r"\s*(\w+)\s*(?:\[(\d+)\])?", name)
+            n += int(m.group(2)) if m.group(2) else 1
+    assert ctypes.sizeof(_lib.Stats) == 8 * n
 
 
 def test_library_is_gfx950_code_object():

@@ -1,0 +1,86 @@
+"""GPU: the batch entry points' many-floods mode (msg_set_batch_floods: every frame of the call in
+one k_serial_multi launch, one wave per flood) against the C oracle, frame by frame.  The frames
+are the serial regime the mode is for -- scattered notConnectedMarkers-style seeds, uniform noise,
+an album.jpg crop with the shape method's seeds -- plus a plateau mosaic (mode 2 hands it back to
+the full engine) and degenerate sizes."""
+import os
+
+import numpy as np
+import pytest
+
+from msegment import synth
+from oracle import ws_oracle
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def frames():
+    out = []
+    for kind, H, W, seed in (("random", 96, 128, 1), ("mosaic_noise", 128, 128, 2), ("mosaic", 160, 96, 3),
+                             ("random", 3, 3, 4), ("random", 1, 7, 5), ("mosaic_noise", 61, 257, 6)):
+        img, m, _ = synth.frame(kind, H, W, seed)
+        out.append((img, m))
+    rng = np.random.default_rng(7)
+    img = synth.frame("mosaic_noise", 200, 200, 8)[0]
+    m = np.where(rng.random((200, 200)) < 0.02, rng.integers(1, 9, (200, 200)), 0).astype(np.int32)
+    out.append((img, m))  # scattered seeds with few labels: the NC pipeline's kind of markers
+    from PIL import Image
+    rgb = np.asarray(Image.open(os.path.join(ROOT, "tests", "golden", "album_1500x1500.png")).convert("RGB"))
+    album = np.ascontiguousarray(rgb[200:456, 300:620, ::-1])
+    m = np.zeros(album.shape[:2], np.int32)
+    m[::37, ::41] = np.arange(1, m[::37, ::41].size + 1).reshape(m[::37, ::41].shape)
+    out.append((album, m))
+    return out
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_batch_many_host_buffers(seg, mode):
+    fr = frames()
+    work = [m.copy() for _, m in fr]
+    seg.set_batch_floods(mode)
+    try:
+        seg.watershed_batch([(img, w) for (img, _), w in zip(fr, work)])
+    finally:
+        seg.set_batch_floods(0)
+    for k, ((img, m), got) in enumerate(zip(fr, work)):
+        assert np.array_equal(got, ws_oracle.watershed(img, m)), k
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_batch_many_device(seg, mode):
+    import torch
+
+    dev = torch.device("cuda", seg.device)
+    fr = [f for f in frames() if f[1].size > 0]
+    depth = 64
+    imgs = [torch.from_numpy(img).to(dev) for img, _ in fr]
+    mks = [torch.from_numpy(m).to(dev) for _, m in fr]
+    labs = [torch.empty_like(x) for x in mks]
+    dsts = [torch.empty(img.shape, dtype=torch.uint8, device=dev) for img, _ in fr]
+    seg.set_batch_floods(mode)
+    try:
+        seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)
+    finally:
+        seg.set_batch_floods(0)
+    torch.cuda.synchronize()
+    for k, (img, m) in enumerate(fr):
+        want = ws_oracle.watershed(img, m)
+        assert np.array_equal(labs[k].cpu().numpy(), want), k
+        assert np.array_equal(dsts[k].cpu().numpy(), ws_oracle.colorize(want, depth, None)), k
+        assert np.array_equal(mks[k].cpu().numpy(), m), k  # inputs untouched
+
+
+def test_batch_many_repeat_and_grow(seg):
+    """Two calls in a row on the same context (workspaces reused), the second with more frames."""
+    fr = frames()
+    seg.set_batch_floods(1)
+    try:
+        for n in (3, len(fr)):
+            work = [m.copy() for _, m in fr[:n]]
+            seg.watershed_batch([(img, w) for (img, _), w in zip(fr[:n], work)])
+            for k in range(n):
+                assert np.array_equal(work[k], ws_oracle.watershed(*fr[k])), (n, k)
+    finally:
+        seg.set_batch_floods(0)
