@@ -56,6 +56,8 @@ struct msg_ctx {
   unsigned long long *d_stl = nullptr, *d_slog = nullptr;
   unsigned long long *d_ssig = nullptr, *d_stmp = nullptr, *d_sflag = nullptr, *d_sxp = nullptr;
   long long spec_xcap = 0;       // d_sxp entries (k_spec_round's per-round chunk pool)
+  int spec_maxrec = SPEC_MAXREC_SHORT;  // pops per execution before it overflows, until the flood's
+                                       // SPEC_FB_LONG-th fallback (MSEG_SPEC_MAXREC overrides)
   int4* d_srec = nullptr;
   int2* d_sfrec = nullptr;
   unsigned* d_sdirt = nullptr;
@@ -77,6 +79,8 @@ struct msg_ctx {
   unsigned epoch = 1;
   int group = 8;
   int res_grid = 0;   // k_resolve blocks per launch (occupancy x CUs by default; a perf knob)
+  int commit_subs = FAST_SUBS;  // k_commit_fast sub-round blocks: the whole chip, or a share of it
+                                // per flood when a batch keeps several in flight (run_batch)
   msg_stats stats{};
   // optional per-kernel HIP-event profiling (msg_set_profiling)
   bool prof = false;
@@ -397,6 +401,7 @@ void bind_spec(msg_ctx* c, FloodRun& fr, bool on) {
   ws.sdirt = on ? c->d_sdirt : nullptr;
   ws.sxp = on ? c->d_sxp : nullptr;
   ws.sxcap = on ? std::min<long long>(c->spec_xcap, 0x7fffffffll) : 0;
+  ws.spec_maxrec = c->spec_maxrec;
   ws.snp = on ? c->spec_np : 0;
   ws.slogcap = on ? c->spec_logcap : 0;
   ws.spec_lazy = (fr.spec && !on) ? 1 : 0;
@@ -538,6 +543,8 @@ int flood_loop(msg_ctx* c, FloodRun& fr) {
           LAUNCH(c, KID_RESOLVE, st, k_resolve<false>, dim3(gres), dim3(RBS), 0, ws);
         if (c->h_mir[6] == 2)  // the last report was a batch above FAST_CH chunks
           LAUNCH(c, KID_COMMIT_FAST, st, k_commit_fast_mp, dim3(FAST_SUBS + 1), dim3(1024), 0, ws, it);
+        else if (c->commit_subs < FAST_SUBS)  // a share of the chip: FAST_PASS sub-rounds per block
+          LAUNCH(c, KID_COMMIT_FAST, st, k_commit_fast_mp, dim3(c->commit_subs + 1), dim3(1024), 0, ws, it);
         else
           LAUNCH(c, KID_COMMIT_FAST, st, k_commit_fast, dim3(FAST_SUBS + 1), dim3(1024), 0, ws, it);
         continue;
@@ -731,7 +738,17 @@ int run_batch(msg_ctx* c, int n, F fn) {
   // runtime's hardware queues share them and serialise).  Concurrent k_resolve grids need not be
   // co-resident (a block waiting on an unclaimed chunk gives its own chunk up and the batch is
   // re-run, ws_kernels.hip), so each flood keeps the full grid.
+  // k in flight: each flood's commit grid takes a 1/k share of the chip (its blocks then take up
+  // to FAST_PASS sub-rounds each), so that concurrent floods' commits overlap instead of each
+  // filling every wave slot; at least FAST_SUBS / FAST_PASS blocks (the batches reported as
+  // fitting FAST_CH chunks still fit).  MSEG_BATCH_COMMIT_SUBS overrides (A/B runs).
+  int csubs = std::max(FAST_SUBS / FAST_PASS, (FAST_SUBS / k) / (CH / 1024) * (CH / 1024));
+  if (const char* e = getenv("MSEG_BATCH_COMMIT_SUBS")) {
+    const int v = atoi(e);
+    if (v > 0) csubs = std::max(FAST_SUBS / FAST_PASS, std::min(FAST_SUBS, v / (CH / 1024) * (CH / 1024)));
+  }
   for (int w = 0; w < k; ++w) {
+    c->subs[w]->commit_subs = csubs;
     c->subs[w]->res_grid = c->res_grid;
     c->subs[w]->spec = c->spec;
     c->subs[w]->fast = c->fast;
@@ -1072,6 +1089,8 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
   msg_ctx* c = new (std::nothrow) msg_ctx();
   if (!c) return MSG_ENOMEM;
   c->dev = device_ordinal;
+  if (const char* e = getenv("MSEG_SPEC_MAXREC"))  // A/B knob: the execution length cap
+    c->spec_maxrec = std::max(1, std::min(atoi(e), SPEC_MAXREC));
   // MSEG_STREAM_PRIORITY=high|low: the context's stream at that priority (a tuning knob for
   // concurrent floods: the HIP runtime keeps streams of different priorities on different
   // hardware queues)

@@ -46,7 +46,7 @@ constexpr unsigned SPEC_RMAX = (1u << 22) - 1;
 #define MSEG_SPEC_MINB 2  // two blocks per CU (the LDS allows two): caps the registers at 256
 #endif
 #ifndef MSEG_SPEC_RFW
-#define MSEG_SPEC_RFW 2
+#define MSEG_SPEC_RFW 8
 #endif
 constexpr int SPEC_RFW = MSEG_SPEC_RFW;  // cold keys loaded together in a refill pass
 static_assert(SPEC_NX == 4, "k_spec_round keeps SPEC_NX record chunk bases in four registers");
@@ -230,6 +230,11 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
   if (tid == 0) s_exec = s_rep = 0;
   const unsigned T = ctl->spec.T, G = ctl->spec.G;
   const int P = ctl->spec.P, n = ctl->spec.n, L = ctl->spec.L, bstart = ctl->spec.bstart;
+  // An execution may run ws.spec_maxrec pops (a lane's cascade pop costs several times a serial
+  // pop, so long cascades are cheaper as serial pops); a flood that keeps falling back (uniform
+  // noise at 4096^2: invasion-percolation avalanches of thousands of pops, every generation cut)
+  // lets its executions run to SPEC_MAXREC instead, the lanes' cost being less than the re-runs
+  const int reccap = ctl->spec.fallbacks >= SPEC_FB_LONG ? SPEC_MAXREC : ws.spec_maxrec;
   const int par = (int)(T & 1u), ppar = (int)((T - 1u) & 1u);
   // replays need complete change marks: no overflowing execution (claims never logged in full)
   // below the item in the last two rounds
@@ -433,6 +438,7 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
       int nq = 0, nc = 0;   // hot / cold keys
       int cb = -1;          // cold chunk in ws.sxp
       unsigned cmin = 256;  // lowest level among the cold keys
+      unsigned long long hmx = 0;  // largest hot key (pops take the smallest: it stays valid)
       unsigned qseq = 0;    // pushes of this execution
       auto pool_get = [&](int sz) -> int {
         const int b = atomicAdd(&ctl->sxtop.v, sz);
@@ -463,23 +469,22 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
         }
         if (nq < SPEC_QCAP) {
           lq[(nq++) * SPEC_BS + tid] = k;
+          hmx = max(hmx, k);
           return;
         }
-        int mi = 0;  // hot is full: the larger of k and the largest hot key goes cold
-        unsigned long long mk = lq[tid];
-        for (int e = 1; e < SPEC_QCAP; ++e) {
-          const unsigned long long v = lq[e * SPEC_BS + tid];
-          if (v > mk) {
-            mk = v;
-            mi = e;
-          }
-        }
-        if (k > mk) {
+        if (k > hmx) {  // hot is full: the larger of k and the largest hot key goes cold
           cold_add(k);
-        } else {
-          cold_add(mk);
-          lq[mi * SPEC_BS + tid] = k;
+          return;
         }
+        int mi = 0;
+        #pragma unroll 1
+        for (int e = 1; e < SPEC_QCAP; ++e)
+          if (lq[e * SPEC_BS + tid] == hmx) mi = e;
+        cold_add(hmx);
+        lq[mi * SPEC_BS + tid] = k;
+        hmx = k;
+        #pragma unroll 1
+        for (int e = 0; e < SPEC_QCAP; ++e) hmx = max(hmx, lq[e * SPEC_BS + tid]);
       };
       // hot empty, cold not: the SPEC_QCAP smallest cold keys become hot (one pass keeping the
       // smallest seen, one pass compacting the rest in place)
@@ -487,6 +492,7 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
         const size_t b = (size_t)cb;
         unsigned long long hmax = 0;
         int hmi = 0;
+        #pragma unroll 1
         for (int k0 = 0; k0 < nc; k0 += SPEC_RFW) {
           unsigned long long v[SPEC_RFW];
   #pragma unroll
@@ -504,6 +510,7 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
             } else if (v[k] < hmax) {
               lq[hmi * SPEC_BS + tid] = v[k];
               hmax = 0;
+              #pragma unroll 1
               for (int e = 0; e < SPEC_QCAP; ++e) {
                 const unsigned long long u = lq[e * SPEC_BS + tid];
                 if (u > hmax) {
@@ -514,8 +521,10 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
             }
           }
         }
+        hmx = hmax;
         int w = 0;
         cmin = 256;
+        #pragma unroll 1
         for (int k0 = 0; k0 < nc; k0 += SPEC_RFW) {
           unsigned long long v[SPEC_RFW];
   #pragma unroll
@@ -591,6 +600,7 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
         }
         --nq;
         lq[bi * SPEC_BS + tid] = lq[nq * SPEC_BS + tid];
+        if (nq == 0) hmx = 0;
         return (int)(be & 0x0fffffffull);
       };
       int y = 0;
@@ -614,6 +624,10 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
       }
       if (py >= 0) issue_writes(0);
       while (more) {
+        if (nrec >= reccap) {  // a long cascade: cheaper as serial pops
+          ovf = cap = true;
+          break;
+        }
         if (nrec >= SPEC_RL && (nrec - SPEC_RL) % SPEC_XCH == 0) {  // the next record starts a chunk
           const int c = (nrec - SPEC_RL) / SPEC_XCH;
 #ifdef MSEG_SPEC_NOSPILL
@@ -927,6 +941,9 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
       // judged on the generations' own time (+ a commit estimate each) per pop they committed,
       // not on the wall time since the regime started: a fallback's serial pops cost the same
       // either way (round 3 A/B: neutral on every frame, profiles/r03l_ab_regimes.log)
+      // (leaving the generations that fell back out of this judgement kept the regime on where it
+      // re-ran the rest of a bucket after every long cascade: uniform noise at 4096^2 went from 15.7
+      // to 48 s, round 4)
       s.tspec += now - s.tgen + SPEC_COMMIT_TICKS;
       s.pspec += Vn;
       const bool slow = judge && s.tspec > (long long)SPEC_SERIAL_TICKS * s.pspec;

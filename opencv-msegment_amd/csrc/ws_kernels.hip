@@ -1782,14 +1782,14 @@ __device__ __forceinline__ int rows_sum_any(const int* cnt, int g, int nrows, in
 // What the commit of the current batch is: 1 commit ncommit items, 2 re-run (a k_resolve block
 // gave its chunk up), 4 decided but too large (k_scan commits it), 0 nothing to do.
 template <bool MP>
-__device__ __forceinline__ int fast_flags(const Ctl* ctl, const Batch& B, int& ncommit) {
+__device__ __forceinline__ int fast_flags(const Ctl* ctl, const Batch& B, int& ncommit, int G) {
   const unsigned rsv = ctl->rsv, hold = ctl->hold;
   const int err = ctl->error, give = ctl->rgive, cut = ctl->cut, segcut = ctl->segcut;
   ncommit = 0;
   const bool decided = B.mode == 0 && B.n > 0 && rsv == B.epoch && !err && hold != B.epoch;
   if (!decided) return 0;
   if (give) return 2;
-  if (B.n > (MP ? FAST_PASS : 1) * FAST_CH * CH) return 4;
+  if (B.n > (MP ? FAST_PASS : 1) * G * 1024) return 4;  // G sub-round blocks of 1024 items
   ncommit = B.n;
   if (cut != NONE) ncommit = min(ncommit, cut + 1);
   if (segcut != NONE) ncommit = min(ncommit, ctl->seg[segcut].rank);
@@ -1807,6 +1807,9 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
   __shared__ int s_ncommit, s_flags;
   const int tid = threadIdx.x, wv = tid >> 6;
   const int Wt = ws.Wt;
+  // G sub-round blocks (the grid is G + 1; G a multiple of SUBS, at most FAST_SUBS): the whole
+  // chip for one flood, a share of it per flood when the batch entry points keep several in flight
+  const int G = (int)gridDim.x - 1;
   // the bucket bases are loaded into registers before the header: a global -> LDS copy after
   // thread 0's header branch would cost wave 0 a second round trip before the barrier
 #ifdef MSEG_CF_PROF
@@ -1822,7 +1825,7 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
   if (tid == 0) {
     const Batch B = ctl->bat;
     int ncommit;
-    s_flags = fast_flags<MP>(ctl, B, ncommit);
+    s_flags = fast_flags<MP>(ctl, B, ncommit, G);
     s_ncommit = ncommit;
     s_B = B;
   }
@@ -1832,27 +1835,27 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
   const Batch B = s_B;
   const int ncommit = s_ncommit, flags = s_flags;
   unsigned* const arrive = (unsigned*)&ctl->farrive[0];
-  if (blockIdx.x < FAST_SUBS) {
+  if ((int)blockIdx.x < G) {
     // ---- a sub-round block ----
     const int vb = blockIdx.x, ch = vb / SUBS, i0 = ch * CH + (vb % SUBS) * 1024;
     if (!(flags & 1) || i0 >= ncommit) {  // block-uniform: nothing to scatter, done reading
       if (tid == 0) atomicAdd(&arrive[blockIdx.x & 7], 1u);
       return;
     }
-    // Sub-rounds vb, vb + FAST_SUBS, ... (up to FAST_PASS of them: batches of up to FAST_PASS *
-    // FAST_CH chunks).  First, for each of them, everything the finalizer will rewrite -- the old
+    // Sub-rounds vb, vb + G, ... (up to FAST_PASS of them: batches of up to FAST_PASS * G / SUBS
+    // chunks).  First, for each of them, everything the finalizer will rewrite -- the old
     // tails and the earlier chunks' histogram rows -- is read and reduced to the sub-round's
     // starting offsets per level (s_run); then the block arrives, and the scatters follow (their
     // descriptors, items and granules are the batch's, which only the next k_resolve rewrites).
-    // pass j's chunk is FAST_CH chunks after pass j - 1's: its row prefix adds one window of
-    // FAST_CH rows (one round trip) to the previous one
+    // pass j's chunk is G / SUBS (<= FAST_CH) chunks after pass j - 1's: its row prefix adds one
+    // window of G / SUBS rows (one round trip) to the previous one
     int acc = (tid < NQ) ? ctl->qtail[tid] : 0;
     int npass = 0;
 #pragma unroll 1
     for (int j = 0; j < NPASS; ++j) {
-      const int vs = vb + j * FAST_SUBS, chj = vs / SUBS;
+      const int vs = vb + j * G, chj = vs / SUBS;
       if (chj * CH + (vs % SUBS) * 1024 >= ncommit) break;  // block-uniform
-      const int c0 = (j == 0) ? 0 : chj - FAST_CH;
+      const int c0 = (j == 0) ? 0 : chj - G / SUBS;
       gpart[tid >> 8][tid & (NQ - 1)] = rows_sum(ws.cnt + (long long)c0 * NQ, tid >> 8, chj - c0, tid & (NQ - 1));
       __syncthreads();
       if (tid < NQ) {
@@ -1869,7 +1872,7 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
 #endif
 #pragma unroll 1
     for (int j = 0; j < npass; ++j) {
-      const int vs = vb + j * FAST_SUBS, chj = vs / SUBS, sub = vs % SUBS;
+      const int vs = vb + j * G, chj = vs / SUBS, sub = vs % SUBS;
       const int i0j = chj * CH + sub * 1024;
       // the earlier sub-rounds' descriptors of its chunk and its own items: one round trip
       unsigned long long dj[SUBS - 1];
@@ -1995,7 +1998,7 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
   // read the next batch's words).  The grid fits the device at once (FAST_SUBS + 1 blocks of 1024
   // threads, two per CU), and sub-round blocks never wait, so they all get to run.
   if (tid < 64) {
-    const int expect = FAST_SUBS;
+    const int expect = G;
     long long t0 = 0;
     for (;;) {
       unsigned v = (tid < 8) ? __hip_atomic_load(&arrive[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
@@ -2757,7 +2760,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
 constexpr int SER_RING = 16;
 
 struct SerStat {
-  long long pops = 0, pushes = 0;
+  long long pops = 0, pushes = 0, fills = 0;  // fills: ser_run_w's window loads
   unsigned long long tsel = 0, tld = 0, tpush = 0;  // MSEG_SER_PROF: s_memtime cycles per phase
 };
 // the previous pop's writes, not yet issued: the label of pixel pp, and its pushes by direction
@@ -2932,6 +2935,175 @@ __device__ __forceinline__ void ser_run(const Ws& ws, int4* s_bk, int (*s_bring)
   ser_flush(ws, mkb, dummy, P);
 }
 
+// ser_run_w: the same pop loop with the states and weights of a window of SER_WT x SER_WT tiles
+// (48 x 48 pixels) around the pops held in LDS.  cv::watershed's serial regime is local -- an
+// interrupt pops what the last pop pushed, a bucket's FIFO neighbours were pushed by neighbours
+// (scripts/exp/window_hits.c: 76% of album.jpg's pops and 65% of uniform noise's have their
+// neighbourhood in a 24 x 24 window around the last miss) -- so most pops read their four
+// neighbours and weights from LDS (one LDS round trip) instead of memory (one ~1 us round trip
+// for a lone wave).  Writes go through: to memory (every lane the same value, one request) and
+// to the window.  A pop whose neighbourhood leaves the window reloads it centred on the pop: one
+// round trip for the whole window (12 tile rows, each a contiguous run of states and of weights),
+// issued after this wave's earlier stores, so it reads what they wrote.  Bucket bookkeeping as in
+// ser_run; the popped bucket's record lives in scalar registers while the loop stays on it.
+constexpr int SER_WT = 12;  // window tiles per side (4 x 4 pixels each)
+#ifndef MSEG_SER_WINDOW
+#define MSEG_SER_WINDOW 0  // 1: k_serial / k_serial_multi pop with ser_run_w (measured slower, round 4)
+#endif
+__device__ __forceinline__ void ser_run_w(const Ws& ws, int4* s_bk, int (*s_bring)[SER_RING], unsigned long long* ne,
+                                          int& err, SerStat& S, int spec_block, long long cool_lim, int run_limit,
+                                          int* win_s, int* win_w) {
+  const int lane = lane_id();
+  const int Wt = ws.Wt, marg = ws.marg;
+  const int Ht = (ws.H + 3) >> 2;
+  int* const mkb = ws.mk - marg;
+  const int* const mkf = ws.mk;  // frame-relative tiled states / weights
+  const int* const w4f = ws.w4;
+  unsigned long long ne0 = ne[0], ne1 = ne[1], ne2 = ne[2], ne3 = ne[3];
+  int ring = 0, ring_l = -1, ring_h0 = 0, ring_n = 0, run = 0;
+  const double invWt = 1.0 / (double)Wt;
+  int wr0 = -1, wc0 = 0;  // window origin (tile row, tile col); wr0 < 0: none loaded yet
+  // the popped bucket's record {head, tail, base, tail at entry} in registers (cur < 0: none)
+  int cur = -1, ch = 0, ctl_ = 0, cqb = 0, cbe = 0;
+  for (;;) {
+    const unsigned long long t0 = ser_clock();
+    const int lo = ne0 ? __builtin_ctzll(ne0) : ne1 ? 64 + __builtin_ctzll(ne1)
+                 : ne2 ? 128 + __builtin_ctzll(ne2) : ne3 ? 192 + __builtin_ctzll(ne3) : NQ;
+    if (lo >= NQ || run >= run_limit) break;
+    if (spec_block > 0 && lo >= spec_block) break;  // the cascade that stopped the speculative engine is done
+    if (S.pops >= cool_lim) break;                  // its cooldown is over
+    if (ws.spec_lazy && S.pops >= 4096) break;      // the engine is being allocated: let it take over
+    if (lo != cur) {
+      if (cur >= 0 && lane == 0) s_bk[cur] = make_int4(ch, ctl_, cqb, cbe);
+      const int4 rec = s_bk[lo];
+      cur = lo;
+      ch = uni(rec.x);
+      ctl_ = uni(rec.y);
+      cqb = uni(rec.z);
+      cbe = uni(rec.w);
+    }
+    const int h = ch;
+    int p;
+    if (h >= cbe && h >= ctl_ - SER_RING) {  // pushed by this launch: its LDS ring
+      p = uni(s_bring[lo][h & (SER_RING - 1)]);
+    } else if (lo == ring_l && h >= ring_h0 && h < ring_h0 + ring_n) {
+      p = __builtin_amdgcn_readlane(ring, h - ring_h0);
+    } else {  // the bucket's next 64 slots, one load per lane
+      ring_l = lo;
+      ring_h0 = h;
+      ring_n = min(ctl_ - h, 64);
+      ring = (lane < ring_n) ? __hip_atomic_load(ws.qbuf + cqb + h + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                             : 0;
+      p = __builtin_amdgcn_readlane(ring, 0);
+    }
+    const unsigned long long t1 = ser_clock();
+    // p's tile; the window holds p's 3 x 3 tile neighbourhood (where it exists) or is reloaded
+    const int T = p >> 4;
+    int tr = (int)((double)T * invWt);
+    if (tr * Wt > T) --tr;
+    else if ((tr + 1) * Wt <= T) ++tr;
+    tr = uni(tr);
+    const int tc = T - tr * Wt;
+    const bool hit = wr0 >= 0 && tr - (tr > 0 ? 1 : 0) >= wr0 && tr + (tr + 1 < Ht ? 1 : 0) < wr0 + SER_WT &&
+                     tc - (tc > 0 ? 1 : 0) >= wc0 && tc + (tc + 1 < Wt ? 1 : 0) < wc0 + SER_WT;
+    if (!hit) {
+      wr0 = max(0, min(tr - SER_WT / 2, Ht - SER_WT));
+      wc0 = max(0, min(tc - SER_WT / 2, Wt - SER_WT));
+      const int nr = min(SER_WT, Ht - wr0), nc4 = min(SER_WT, Wt - wc0) * 4;  // int4 per window tile row
+      int4 vs[SER_WT], vw[SER_WT];
+#pragma unroll
+      for (int i = 0; i < SER_WT; ++i) {  // every row of both planes in flight together
+        const bool on = i < nr && lane < nc4;
+        const long long g = ((long long)(wr0 + i) * Wt + wc0) * 16 + 4 * lane;
+        vs[i] = on ? *reinterpret_cast<const int4*>(mkf + g) : make_int4(0, 0, 0, 0);
+        vw[i] = on ? *reinterpret_cast<const int4*>(w4f + g) : make_int4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < SER_WT; ++i) {
+        if (i < nr && lane < nc4) {
+          *reinterpret_cast<int4*>(win_s + (i * SER_WT * 16 + 4 * lane)) = vs[i];
+          *reinterpret_cast<int4*>(win_w + (i * SER_WT * 16 + 4 * lane)) = vw[i];
+        }
+      }
+      ++S.fills;
+    }
+    // p and its four neighbours in the window (the same tiled neighbour rule, window-wide rows)
+    const int wb = ((tr - wr0) * SER_WT + (tc - wc0)) * 16 + (p & 15);
+    int wn[4], st[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) wn[d] = nbi(wb, d, SER_WT);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) st[d] = uni(win_s[wn[d]]);
+    const unsigned w4 = (unsigned)uni(win_w[wb]);
+    int lab = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      if (st[d] > 0) lab = fold_lab(lab, st[d]);
+    if (lab == 0) {  // impossible for an exact queue
+      err |= ERR_STATE;
+      lab = WSHED;
+    }
+    const int pb = p + marg;
+    mkb[pb] = lab;
+    if (lane == 0) win_s[wb] = lab;
+    ch = h + 1;
+    ++S.pops;
+    const unsigned long long t2 = ser_clock();
+    bool lower = false, lo_left = h + 1 < ctl_;
+    if (lab != WSHED) {
+      // the push targets' bucket records, all in one LDS round trip (the popped bucket's is in
+      // registers)
+      int4 tr4[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) tr4[d] = s_bk[(w4 >> (8 * d)) & 255u];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        if (st[d] != 0) continue;
+        const int t = (int)((w4 >> (8 * d)) & 255u);
+        int tt = (t == cur) ? ctl_ : uni(tr4[d].y);
+        const int qbt = (t == cur) ? cqb : uni(tr4[d].z);
+        // an earlier push of this pop into the same bucket advanced its tail
+#pragma unroll
+        for (int e = 0; e < d; ++e)
+          if (st[e] == 0 && (int)((w4 >> (8 * e)) & 255u) == t && t != cur) ++tt;
+        const int dest = qbt + tt;
+        if (dest < 0 || (long long)dest >= ws.qcap) {
+          err |= ERR_CAPACITY;
+          continue;
+        }
+        const int nb = nbi(pb, d, Wt);
+        const int qs = queued_state(dest);
+        ws.qbuf[dest] = nb - marg;
+        mkb[nb] = qs;
+        if (lane == 0) {
+          win_s[wn[d]] = qs;
+          s_bring[t][tt & (SER_RING - 1)] = nb - marg;
+          if (t != cur) s_bk[t].y = tt + 1;
+        }
+        if (t == cur) ctl_ = tt + 1;
+        ser_mark(ne0, ne1, ne2, ne3, t, true);
+        ++S.pushes;
+        lower = lower || t < lo;
+        lo_left = lo_left || t == lo;
+      }
+    }
+    if (!lo_left) ser_mark(ne0, ne1, ne2, ne3, lo, false);
+    run = lower ? 0 : run + 1;
+#ifdef MSEG_SER_PROF
+    const unsigned long long t3 = ser_clock();
+    S.tsel += t1 - t0;
+    S.tld += t2 - t1;
+    S.tpush += t3 - t2;
+#else
+    (void)t0;
+    (void)t1;
+    (void)t2;
+#endif
+    if (err) break;
+  }
+  if (cur >= 0 && lane == 0) s_bk[cur] = make_int4(ch, ctl_, cqb, cbe);
+}
+
 __global__ __launch_bounds__(64) void k_serial(Ws ws, int iter) {
   Ctl* ctl = ws.ctl;
   __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ];
@@ -2963,7 +3135,12 @@ __global__ __launch_bounds__(64) void k_serial(Ws ws, int iter) {
     const unsigned long long c_start = ser_clock();
     SerStat S;
     int err = 0;
+#if MSEG_SER_WINDOW
+    __shared__ int s_win[2][SER_WT * SER_WT * 16];
+    ser_run_w(ws, s_bk, s_bring, s_ne, err, S, spec_block, cool_lim, SERIAL_RUN, s_win[0], s_win[1]);
+#else
     ser_run(ws, s_bk, s_bring, s_ne, err, S, spec_block, cool_lim);
+#endif
     wave_sync();
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -2984,6 +3161,7 @@ __global__ __launch_bounds__(64) void k_serial(Ws ws, int iter) {
       atomicAdd(&ws.diag[22], ser_clock() - c_start);
 #else
       (void)c_start;
+      atomicAdd(&ws.diag[22], (unsigned long long)S.fills);
 #endif
     }
     wave_sync();
@@ -3094,7 +3272,12 @@ __global__ __launch_bounds__(64) void k_serial_multi(const Ws* __restrict__ wss,
   wave_sync();
   SerStat S;
   int err = 0;
+#if MSEG_SER_WINDOW
+  __shared__ int s_win[2][SER_WT * SER_WT * 16];
+  ser_run_w(ws, s_bk, s_bring, s_ne, err, S, 0, 1ll << 62, run_limit, s_win[0], s_win[1]);
+#else
   ser_run(ws, s_bk, s_bring, s_ne, err, S, 0, 1ll << 62, run_limit);
+#endif
   wave_sync();
 #pragma unroll
   for (int k = 0; k < 4; ++k) {

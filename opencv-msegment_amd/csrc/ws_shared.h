@@ -81,6 +81,12 @@ constexpr int SPEC_RL = MSEG_SPEC_RL;      // records per execution in lane scra
 constexpr int SPEC_CCAP = 4096;     // "cold" cascade entries of one execution (a pool chunk): more = overflow
 constexpr int SPEC_XCH = 2048;      // records per pool chunk past the first SPEC_RL
 constexpr int SPEC_NX = 4;          // such chunks per execution: more records = overflow
+constexpr int SPEC_MAXREC = SPEC_RL + SPEC_NX * SPEC_XCH;  // longest execution a lane runs
+#ifndef MSEG_SPEC_MAXREC_SHORT
+#define MSEG_SPEC_MAXREC_SHORT 256
+#endif
+constexpr int SPEC_MAXREC_SHORT = MSEG_SPEC_MAXREC_SHORT;  // ... before a flood's SPEC_FB_LONG-th fallback
+constexpr int SPEC_FB_LONG = 8;
 constexpr int SPEC_ROUNDS_MAX = 64; // rounds per generation before the stable prefix is committed
 constexpr int SPEC_FT = 1024;       // items per k_spec_flatten tile
 constexpr int SPEC_QUIET = 4096;    // a generation this large without a cascade ends the regime
@@ -238,6 +244,7 @@ struct Ws {
   unsigned long long* sxp;   // chunk pool of a round: an execution's cold cascade queue (SPEC_CCAP
                              // keys) and its records past SPEC_RL (SPEC_XCH each), reset every round
   long long sxcap;
+  int spec_maxrec;           // pops an execution may run (more: a capacity overflow -> serial pops)
   long long snp;
   long long slogcap;
   int spec_lazy;     // 1: engine enabled, workspace not allocated yet (k_scan reports spec_want)
