@@ -66,6 +66,14 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")  # scripts/pmc_s
 E2E_BYTES_PER_PIXEL = 14.0                  # 3 B BGR + 4 B markers in, 4 B labels + 3 B BGR out
 
 
+def frame_seed(seed, rank, world):
+    """The frame a rank segments: --seed, else config 3's seed 2 on one GPU, else config 5's frame
+    100 + rank (frames 100 + k; replicas, one frame stream per GPU, no collectives)."""
+    if seed is not None:
+        return seed
+    return 2 if world == 1 else 100 + rank
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -678,7 +686,7 @@ def main(argv=None):
     sync = torch.cuda.synchronize
 
     S = args.size
-    seed = args.seed if args.seed is not None else (2 if world == 1 else 100 + rank)
+    seed = frame_seed(args.seed, rank, world)
     # the workload the PMC passes must have been collected on for their traffic to be quoted
     pmc_cfg = {"pipeline": args.pipeline, "kind": args.kind, "size": S, "seed": seed, "frames": max(1, args.frames)}
     t0 = time.perf_counter()

@@ -56,8 +56,9 @@ struct msg_ctx {
   unsigned long long *d_stl = nullptr, *d_slog = nullptr;
   unsigned long long *d_ssig = nullptr, *d_stmp = nullptr, *d_sflag = nullptr, *d_sxp = nullptr;
   long long spec_xcap = 0;       // d_sxp entries (k_spec_round's per-round chunk pool)
-  int spec_maxrec = SPEC_MAXREC_SHORT;  // pops per execution before it overflows, until the flood's
-                                       // SPEC_FB_LONG-th fallback (MSEG_SPEC_MAXREC overrides)
+  int spec_maxrec = SPEC_MAXREC_SHORT;  // pops per execution before it overflows while no recent
+                                       // generation fell back (MSEG_SPEC_MAXREC overrides)
+  int spec_capmode = 7;          // MSEG_SPEC_CAPMODE (A/B): see k_spec_round
   int4* d_srec = nullptr;
   int2* d_sfrec = nullptr;
   unsigned* d_sdirt = nullptr;
@@ -402,6 +403,7 @@ void bind_spec(msg_ctx* c, FloodRun& fr, bool on) {
   ws.sxp = on ? c->d_sxp : nullptr;
   ws.sxcap = on ? std::min<long long>(c->spec_xcap, 0x7fffffffll) : 0;
   ws.spec_maxrec = c->spec_maxrec;
+  ws.spec_capmode = c->spec_capmode;
   ws.snp = on ? c->spec_np : 0;
   ws.slogcap = on ? c->spec_logcap : 0;
   ws.spec_lazy = (fr.spec && !on) ? 1 : 0;
@@ -619,8 +621,9 @@ int flood_end(msg_ctx* c, FloodRun& fr, int32_t* d_labels, int depth = 0, const 
   c->stats.pops = tail.pops;
   c->stats.items = tail.items;
   c->stats.pushes = tail.pushes;
-  c->stats.fast_pops = tail.fpops;
-  c->stats.fast_pushes = tail.fpushes;
+  // k_commit_fast's share is what the other commit paths leave
+  c->stats.fast_pops = std::max(0ll, tail.pops - tail.s0pops - tail.lpops);
+  c->stats.fast_pushes = std::max(0ll, tail.pushes - tail.spushes - tail.lpushes);
   c->stats.scatter_pops = tail.spops;
   c->stats.scatter_pushes = tail.spushes;
   // when speculative generations ran, diag reports their round split instead (spec_kernels.hip)
@@ -1091,6 +1094,8 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
   c->dev = device_ordinal;
   if (const char* e = getenv("MSEG_SPEC_MAXREC"))  // A/B knob: the execution length cap
     c->spec_maxrec = std::max(1, std::min(atoi(e), SPEC_MAXREC));
+  if (const char* e = getenv("MSEG_SPEC_CAPMODE"))  // A/B knob: when the long cap applies
+    c->spec_capmode = atoi(e);
   // MSEG_STREAM_PRIORITY=high|low: the context's stream at that priority (a tuning knob for
   // concurrent floods: the HIP runtime keeps streams of different priorities on different
   // hardware queues)

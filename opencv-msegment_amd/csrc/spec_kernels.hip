@@ -231,10 +231,13 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
   const unsigned T = ctl->spec.T, G = ctl->spec.G;
   const int P = ctl->spec.P, n = ctl->spec.n, L = ctl->spec.L, bstart = ctl->spec.bstart;
   // An execution may run ws.spec_maxrec pops (a lane's cascade pop costs several times a serial
-  // pop, so long cascades are cheaper as serial pops); a flood that keeps falling back (uniform
-  // noise at 4096^2: invasion-percolation avalanches of thousands of pops, every generation cut)
-  // lets its executions run to SPEC_MAXREC instead, the lanes' cost being less than the re-runs
-  const int reccap = ctl->spec.fallbacks >= SPEC_FB_LONG ? SPEC_MAXREC : ws.spec_maxrec;
+  // pop, so a long cascade is cheaper as serial pops).  But a fallback restarts the rest of the
+  // bucket as a new generation; where long cascades are everywhere (uniform noise at 4096^2:
+  // invasion-percolation avalanches of thousands of pops) those re-runs and the regime's
+  // cooldowns cost far more than slow lanes, so after a fallback executions may run SPEC_MAXREC
+  // pops, until a generation's executions all stay within the short cap again
+  const int capmode = ws.spec_capmode;
+  const bool lcap = capmode == 7 ? ctl->spec.deep != 0 : ctl->spec.longcap != 0;
   const int par = (int)(T & 1u), ppar = (int)((T - 1u) & 1u);
   // replays need complete change marks: no overflowing execution (claims never logged in full)
   // below the item in the last two rounds
@@ -624,7 +627,11 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
       }
       if (py >= 0) issue_writes(0);
       while (more) {
-        if (nrec >= reccap) {  // a long cascade: cheaper as serial pops
+        // the execution length cap (policy: Ws.spec_capmode, an A/B knob)
+        const bool longok = capmode == 1 ? lcap : capmode == 2 ? (T > G) : capmode == 3 ? (j == P)
+                          : capmode == 4 ? (lcap && T > G) : capmode == 5 ? (T > G || j == P)
+                          : capmode == 7 ? (j == P || (lcap && T > G)) : false;
+        if (nrec >= (longok ? SPEC_MAXREC : ws.spec_maxrec)) {  // a long cascade: cheaper as serial pops
           ovf = cap = true;
           break;
         }
@@ -714,6 +721,10 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
       tw += tkb - tka;
       tc += (long long)__builtin_amdgcn_s_memrealtime() - tkb;
       maxrec = max(maxrec, nrec);
+    }
+    {  // the generation's longest execution (SpecCtl.longcap)
+      const int wx = -wave_min(ex ? -nrec : 0);
+      if (lane == 0 && wx > ws.spec_maxrec) atomicMax(&ctl->spec.xmax, wx);
     }
     // ---- log space for the wave's records (one atomic per wave), signatures, change words ----
     const int want = (ex && !ovf && rbase < 0) ? nrec : 0;
@@ -820,6 +831,7 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
   __shared__ int wsum[SPEC_FT / 64];
   if (P == 0) {  // nothing final (overflow at rank 0): the batch engine takes the bucket's head
     if (blockIdx.x == 0 && tid == 0) {
+      s.longcap = 1;
       Batch nb = ctl->bat;
       nb.mode = 0;
       nb.n = min(s.n, WMIN);
@@ -954,11 +966,18 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
         s.on = 0;
         s.block = slow ? 0 : L;
         s.fallbacks += 1;
+        s.longcap = 1;
         ctl->wcap = WMIN;
       } else if (Vn == P && s.n >= SPEC_QUIET) {  // a large generation without a cascade: batches pay
         s.on = 0;
         s.block = 0;
       }
+      if (!s.fallback && s.xmax <= 0) s.longcap = 0;  // every execution within the short cap
+      // judged slower than serial pops: long final cascades serialised one per round as heads of
+      // the stable prefix (uniform noise at 4096^2: invasion-percolation avalanches everywhere).
+      // Besides the cooldown, from here on every execution may run long from round 2 on
+      // (SpecCtl.deep; round 4 A/B: 16.7 -> 1.6 s there, neutral on album.jpg and random 1024^2)
+      if (slow) s.deep = 1;
       if (slow) {
         s.on = 0;
         s.block = 0;

@@ -832,6 +832,7 @@ __device__ void spec_begin(Ctl* ctl, Batch& nb, int L, int bstart, int navail) {
   s.ticket = 0;
   ctl->slogtop.v = 0;
   ctl->sxtop.v = 0;
+  s.xmax = 0;
   s.fallback = 0;
   s.ftile = 0;
   s.tgen = (long long)__builtin_amdgcn_s_memrealtime();
@@ -1555,6 +1556,7 @@ __device__ Batch scan_body(const Ws& ws) {
     if (B.mode == 0) {
       ctl->pops += ncommit;
       ctl->items += B.n;
+      ctl->s0pops += ncommit;
     }
     ctl->spops += ncommit;
     Batch cb = B;
@@ -1809,7 +1811,7 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
   const int Wt = ws.Wt;
   // G sub-round blocks (the grid is G + 1; G a multiple of SUBS, at most FAST_SUBS): the whole
   // chip for one flood, a share of it per flood when the batch entry points keep several in flight
-  const int G = (int)gridDim.x - 1;
+  const int G = MP ? (int)gridDim.x - 1 : FAST_SUBS;  // (compile-time on the single-flood path)
   // the bucket bases are loaded into registers before the header: a global -> LDS copy after
   // thread 0's header branch would cost wave 0 a second round trip before the barrier
 #ifdef MSEG_CF_PROF
@@ -1834,7 +1836,7 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
   CF_STAMP(0);
   const Batch B = s_B;
   const int ncommit = s_ncommit, flags = s_flags;
-  unsigned* const arrive = (unsigned*)&ctl->farrive[0];
+  unsigned* const arrive = &ctl->farrive.v[0];
   if ((int)blockIdx.x < G) {
     // ---- a sub-round block ----
     const int vb = blockIdx.x, ch = vb / SUBS, i0 = ch * CH + (vb % SUBS) * 1024;
@@ -1984,10 +1986,7 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
       atomicAdd(&s_head[r_sg.L], max(0, min(ncommit - r_sg.rank, r_sg.n)));
     if (tid < NQ) {
       dp = wave_sum(dp);
-      if ((tid & 63) == 0 && dp) {
-        atomicAdd((unsigned long long*)&ctl->pushes, (unsigned long long)dp);
-        atomicAdd((unsigned long long*)&ctl->fpushes, (unsigned long long)dp);
-      }
+      if ((tid & 63) == 0 && dp) atomicAdd((unsigned long long*)&ctl->pushes, (unsigned long long)dp);
     }
     __syncthreads();
     form_batch(qb, s_head, s_tail, s_minpush, s_wcap, nsegs, &s_nseg, &s_n);
@@ -2037,7 +2036,6 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
     }
     if (tid == 0) {
       ctl->pops += ncommit;
-      ctl->fpops += ncommit;
       ctl->items += B.n;
       Batch nb;
       nb.mode = 0;
@@ -2347,7 +2345,7 @@ __device__ __forceinline__ int lowest_bucket(const int* head, const int* tail, i
 
 __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qbase, int* s_head, int* s_tail,
                             int* s_wcap, int* s_err, int* s_nseg, int* s_n, int* s_ser, long long* cnt,
-                            int spec_block, int* spec_cool) {
+                            int spec_block, int* spec_cool, int run_limit = SERIAL_RUN) {
   const int lane = lane_id();
   const int Wt = ws.Wt, marg = ws.marg;
   const Batch B0 = *s_B;
@@ -2362,7 +2360,7 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
       lo = lowest_bucket(s_head, s_tail, lo + 1);
       continue;
     }
-    if (run >= SERIAL_RUN) break;
+    if (run >= run_limit) break;
     if (spec_block > 0 && lo >= spec_block) break;  // the cascade that stopped the speculative engine is done
     if (pops >= cool_lim) break;  // its cooldown is over
     // the speculative engine is being allocated (first entry into this regime): return soon, so
@@ -2736,6 +2734,8 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     ctl->pops += nb_pops;
     ctl->items += nb_items;
     ctl->pushes += nb_push;
+    ctl->lpops += nb_pops;
+    ctl->lpushes += nb_push;
     if (s_err) ctl->error |= s_err;
     if (s_B.n == 0 && !s_err) ctl->done = 1;
   }
@@ -3216,6 +3216,8 @@ __global__ __launch_bounds__(64) void k_serial(Ws ws, int iter) {
       ctl->pops += pops;
       ctl->items += pops;
       ctl->pushes += pushes;
+      ctl->lpops += pops;
+      ctl->lpushes += pushes;
       if (s_err) ctl->error |= s_err;
       if (nb.n == 0 && !s_err) ctl->done = 1;
     }
@@ -3246,20 +3248,78 @@ __global__ __launch_bounds__(64) void k_serial(Ws ws, int iter) {
 // nothing below their own level (batches pay again: the host finishes that flood with the full
 // engine), then writes the queue state back and forms the next batch as k_serial does.  No wave
 // waits for another: each block only touches its own flood.
+#ifndef MSEG_MULTI_LOOP
+#define MSEG_MULTI_LOOP 1  // 1: k_scan's serial_loop per flood, 0: k_serial's ser_run (round 4 A/B)
+#endif
 __global__ __launch_bounds__(64) void k_serial_multi(const Ws* __restrict__ wss, int n, int run_limit) {
   const int f = blockIdx.x;
   if (f >= n) return;
   const Ws ws = wss[f];
   Ctl* ctl = ws.ctl;
+  const int lane = lane_id();
+  const Batch B0 = ctl->bat;
+  if (ctl->done || ctl->error || B0.n == 0 || (B0.mode != 0 && B0.mode != 4)) return;
+#if MSEG_MULTI_LOOP
+  // the small-batch loop's own serial pops (queue state in LDS, the bucket's next 64 slots in a
+  // register, stores straight out): the in-loop form measured faster than ser_run's deferred
+  // stores and LDS rings on photographs (album.jpg 1176 against 1362 ms, round 4)
+  __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ];
+  __shared__ Seg s_seg[NQ];
+  __shared__ Batch s_B;
+  __shared__ int s_wcap, s_err, s_nseg, s_n, s_ser;
+#pragma unroll
+  for (int k = 0; k < NQ / 64; ++k) {
+    const int b = 64 * k + lane;
+    s_qbase[b] = ctl->qbase[b];
+    s_head[b] = ctl->qhead[b];
+    s_tail[b] = ctl->qtail[b];
+  }
+  if (lane == 0) {
+    s_B = B0;
+    s_B.mode = 0;
+    s_wcap = 0;
+    s_err = 0;
+    s_ser = 1;
+  }
+  wave_sync();
+  long long cnt[4] = {0, 0, 0, 0};
+  serial_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, cnt, 0, nullptr,
+              run_limit);
+  wave_sync();
+  for (int k = lane; k < NQ; k += 64) {
+    ctl->qhead[k] = s_head[k];
+    ctl->qtail[k] = s_tail[k];
+  }
+  const int ns = s_nseg;
+  for (int k = lane; k < ns; k += 64) ctl->seg[k] = s_seg[k];
+  int q = 0;
+#pragma unroll
+  for (int k = 0; k < NQ / 64; ++k) q += s_tail[lane + 64 * k] - s_head[lane + 64 * k];
+  q = wave_sum(q);
+  if (lane == 0) {
+    const Batch nb = s_B;
+    ctl->bat = nb;
+    ctl->wcap = 0;
+    ctl->cut = NONE;
+    ctl->segcut = NONE;
+    ctl->minpush = NQ;
+    ctl->remaining = q;
+    ctl->batches += cnt[0];
+    ctl->pops += cnt[0];
+    ctl->items += cnt[1];
+    ctl->pushes += cnt[2];
+    ctl->lpops += cnt[0];
+    ctl->lpushes += cnt[2];
+    if (s_err) ctl->error |= s_err;
+    if (nb.n == 0 && !s_err) ctl->done = 1;
+  }
+#else
   __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ];
   __shared__ int s_bring[NQ][SER_RING];
   __shared__ Seg s_seg[NQ];
   __shared__ int s_nseg, s_n;
   __shared__ int4 s_bk[NQ];
   __shared__ unsigned long long s_ne[4];
-  const int lane = lane_id();
-  const Batch B0 = ctl->bat;
-  if (ctl->done || ctl->error || B0.n == 0 || (B0.mode != 0 && B0.mode != 4)) return;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int b = 64 * k + lane;
@@ -3319,9 +3379,12 @@ __global__ __launch_bounds__(64) void k_serial_multi(const Ws* __restrict__ wss,
     ctl->pops += S.pops;
     ctl->items += S.pops;
     ctl->pushes += S.pushes;
+    ctl->lpops += S.pops;
+    ctl->lpushes += S.pushes;
     if (err) ctl->error |= err;
     if (nb.n == 0 && !err) ctl->done = 1;
   }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------

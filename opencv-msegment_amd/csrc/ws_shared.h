@@ -85,8 +85,7 @@ constexpr int SPEC_MAXREC = SPEC_RL + SPEC_NX * SPEC_XCH;  // longest execution 
 #ifndef MSEG_SPEC_MAXREC_SHORT
 #define MSEG_SPEC_MAXREC_SHORT 256
 #endif
-constexpr int SPEC_MAXREC_SHORT = MSEG_SPEC_MAXREC_SHORT;  // ... before a flood's SPEC_FB_LONG-th fallback
-constexpr int SPEC_FB_LONG = 8;
+constexpr int SPEC_MAXREC_SHORT = MSEG_SPEC_MAXREC_SHORT;  // ... except the stable prefix's head
 constexpr int SPEC_ROUNDS_MAX = 64; // rounds per generation before the stable prefix is committed
 constexpr int SPEC_FT = 1024;       // items per k_spec_flatten tile
 constexpr int SPEC_QUIET = 4096;    // a generation this large without a cascade ends the regime
@@ -134,6 +133,11 @@ struct SpecCtl {
   long long gens, rounds_total, execs, cpops, fallbacks;
   unsigned long long rmax;  // diagnostics: longest wave of this round (10 ns ticks)
   int ov1, ov2;             // lowest overflowing rank of the last / the one-before-last round
+  int longcap;              // executions may run SPEC_MAXREC pops (else Ws.spec_maxrec): set by a
+                            // fallback, cleared by a generation whose executions all stayed short
+  int xmax;                 // longest execution (pops) of the current generation, all rounds
+  int deep;                 // sticky, set by the first cooldown: from round 2 on every execution
+                            // may run SPEC_MAXREC pops
   long long replays;        // executions whose cascade was replayed from the previous round
 };
 
@@ -184,8 +188,6 @@ struct Ctl {
   long long pops;
   long long items;   // sum of batch sizes resolved (committed or not)
   long long pushes;  // committed pushes appended to buckets
-  long long fpops, fpushes;  // of which committed by k_commit_fast (the roofline's bytes per launch)
-  long long spops, spushes;  // of which committed by k_scan + k_scatter (batches above SMALL_MAX)
   unsigned rsv;      // epoch of the last batch k_resolve (or k_spec_flatten) decided
   int pad;
   SpecCtl spec;
@@ -193,7 +195,14 @@ struct Ctl {
                      // its workspace not yet allocated (Ws.spec_lazy): the host allocates it
   unsigned hold;     // epoch of a decided batch k_commit_fast declined (k_resolve must not re-run it)
   int pad3;
-  unsigned farrive[8];  // k_commit_fast: sub-round blocks done reading, by blockIdx % 8 (zeroed after)
+  // k_commit_fast: sub-round blocks done reading, by blockIdx % 8 (zeroed after): 480 atomics per
+  // launch and the finalizer's polls, on a line of their own (round 4: sharing one with the batch
+  // words every block reads at its start cost the headline ~4%)
+  struct alignas(128) Arrive {
+    unsigned v[8];
+    unsigned pad[24];
+  };
+  Arrive farrive;
   // k_spec_round's contended words, one 128-B line each: device-scope atomics on one line
   // serialise (~11 ns each), and a round issues thousands of them
   struct alignas(128) Hot {
@@ -204,6 +213,11 @@ struct Ctl {
   Hot sfc, sovf; // lowest changed / overflowing rank of this round
   Hot slogtop;   // generation log records used
   Hot sxtop;     // k_spec_round's chunk pool used this round (cold cascade queues, record chunks)
+  // where the committed items went (bench.py's per-kernel algorithmic bytes), counted off the
+  // critical paths: k_commit_fast's share is what the other paths leave (no atomics in it)
+  long long spops, s0pops, spushes;  // committed by k_scan + k_scatter: all modes, flood batches only
+  long long lpops, lpushes;          // popped one workgroup / one wave at a time (k_scan's loop,
+                                     // k_serial, k_serial_multi)
 };
 
 static_assert(__builtin_offsetof(Ctl, error) % 8 == 0 && __builtin_offsetof(Ctl, rgive) == __builtin_offsetof(Ctl, error) + 4,
@@ -241,22 +255,24 @@ struct Ws {
   unsigned long long* sflag; // k_spec_flatten tile prefixes {generation tag, inclusive sum}
   unsigned* sdirt;           // 2 x snp change marks per round parity: round tag of the last changed
                              // execution whose claims (old or new) covered the pixel
-  unsigned long long* sxp;   // chunk pool of a round: an execution's cold cascade queue (SPEC_CCAP
-                             // keys) and its records past SPEC_RL (SPEC_XCH each), reset every round
-  long long sxcap;
-  int spec_maxrec;           // pops an execution may run (more: a capacity overflow -> serial pops)
   long long snp;
   long long slogcap;
   int spec_lazy;     // 1: engine enabled, workspace not allocated yet (k_scan reports spec_want)
   int serk;          // 1: the serial-pop regime runs in k_serial (mode 4), 0: inside k_scan
-  int multi;         // 1: a flood of a many-floods batch: k_scan stops after each commit (no
-                     // small-batch loop), k_serial_multi pops it together with the others
   int H, W;
   int Wt;            // tiles per tile row = ceil(W / 4)
   int marg;          // tiled entries of margin before mk / w4 (mk - marg starts the state array)
   int nseg;          // raster chunks per image row = ceil(W / RSEG)
   long long N;
   long long qcap;
+  // round 4 (after the fields every flood kernel reads, which keep their offsets)
+  unsigned long long* sxp;   // chunk pool of a round: an execution's cold cascade queue (SPEC_CCAP
+                             // keys) and its records past SPEC_RL (SPEC_XCH each), reset every round
+  long long sxcap;
+  int spec_maxrec;           // pops an execution may run (more: a capacity overflow -> serial pops)
+  int spec_capmode;          // when executions may run SPEC_MAXREC pops instead (k_spec_round)
+  int multi;                 // 1: a flood of a many-floods batch: k_scan stops after each commit (no
+                             // small-batch loop), k_serial_multi pops it together with the others
 };
 
 }  // namespace msg

@@ -11,3 +11,8 @@ timeout -k 10 300 python -u scripts/spec_probe.py random_1024_s3 mosaic_noise_10
 MSEGMENT_LIB=$PWD/$L/libmsegment_specprof.so timeout -k 10 200 python -u scripts/spec_phases.py random_1024_s3 mosaic_noise_1024_s1 > $O/phases.log 2>&1 || exit 1
 bash scripts/ab_bench.sh r04f/ab $L/libmsegment_old.so $L/libmsegment.so > $O/ab.log 2>&1
 echo done
+echo "== many-floods, serial_loop" > $O/many.log
+timeout -k 10 300 python -u scripts/many_probe.py 64 1024 >> $O/many.log 2>&1 || exit 1
+echo "== many-floods, ser_run" >> $O/many.log
+MSEGMENT_LIB=$PWD/$L/libmsegment_multi0.so timeout -k 10 300 python -u scripts/many_probe.py 64 1024 >> $O/many.log 2>&1 || exit 1
+echo done2

@@ -88,6 +88,56 @@ def test_bench_gpus_flag_spawns_ranks():
     assert d["value"] == pytest.approx(2 * 3 / (d["ms_per_step"] * 3 / 1000.0), rel=1e-3)
 
 
+def _replica_worker(rank, world, port, q):
+    """One rank of bench.py's N > 1 layout on CPU: the frame frame_seed gives this rank (config 5's
+    100 + rank), flooded by the C oracle as the stand-in for the GPU step; the labels' digest is
+    gathered to rank 0 -- the only exchange, the data path itself has none."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "opencv-msegment_amd")]
+    import hashlib
+
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    from msegment import synth
+    from oracle import ws_oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    seed = bench.frame_seed(None, rank, world)
+    img, m, _ = synth.frame("mosaic", 4096, 4096, seed)
+    h = hashlib.sha256(ws_oracle.watershed(img, m).tobytes()).hexdigest()
+    mine = torch.tensor(list(bytes.fromhex(h)) + [seed], dtype=torch.int64)
+    got = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(got, mine)
+    if rank == 0:
+        q.put([(int(t[-1]), bytes(t[:-1].tolist()).hex()) for t in got])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_replicas_segment_their_own_config5_frames():
+    """world size 2: rank r floods config 5's frame 100 + r (bench.frame_seed), each digest equals
+    the committed oracle digest of that frame, and the two ranks did different frames."""
+    import json
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_replica_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    dgs = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
+    assert [s for s, _ in res] == [100, 101]
+    for seed, h in res:
+        assert h == dgs["mosaic_4096x4096_s%d" % seed]["labels_sha256"], seed
+
+
 def test_bench_rejects_gpus_world_mismatch():
     import subprocess
 
