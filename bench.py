@@ -392,7 +392,11 @@ def many_floods_line(seg, sync, dev, K, S=1024, steps=2, cpu=True, nc_depth=4):
 
     from msegment import synth
 
-    fr = [synth.frame("mosaic_noise", S, S, 100 + k)[0] for k in range(K)]
+    from concurrent.futures import ThreadPoolExecutor
+
+    # ~0.1 s of numpy hashing per 1024^2 frame: synthesised on the host threads (numpy drops the GIL)
+    with ThreadPoolExecutor(batch_cpu_threads(K)) as ex:
+        fr = list(ex.map(lambda k: synth.frame("mosaic_noise", S, S, 100 + k)[0], range(K)))
     imgs = [torch.from_numpy(f).to(dev) for f in fr]
     mks = [torch.empty((S, S), dtype=torch.int32, device=dev) for _ in fr]
     depth = 1
@@ -427,8 +431,6 @@ def many_floods_line(seg, sync, dev, K, S=1024, steps=2, cpu=True, nc_depth=4):
     out["default_batch_path"] = {"value": round(k8 * S * S / (time.perf_counter() - t0) / 1e6, 3),
                                  "unit": "Mpx/s", "frames": k8, "inflight": 4}
     if cpu:
-        from concurrent.futures import ThreadPoolExecutor
-
         from oracle import ws_oracle
 
         nt = batch_cpu_threads(K)
@@ -646,7 +648,7 @@ def main(argv=None):
     ap.add_argument("--nc-options", default="GISTO_DIAP", help="comma list: GISTO_DIAP,MULTI_OTSU")
     ap.add_argument("--stress-steps", type=int, default=5,
                     help="steps of the config-3 stress line (mosaic+noise at --size); 0 = skip")
-    ap.add_argument("--many-frames", type=int, default=64,
+    ap.add_argument("--many-frames", type=int, default=1024,
                     help="frames of the many-floods line (0: skip it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile-pass", action="store_true")

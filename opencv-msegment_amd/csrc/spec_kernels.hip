@@ -49,6 +49,11 @@ constexpr unsigned SPEC_RMAX = (1u << 22) - 1;
 #define MSEG_SPEC_RFW 8
 #endif
 constexpr int SPEC_RFW = MSEG_SPEC_RFW;  // cold keys loaded together in a refill pass
+#ifndef MSEG_SPEC_HSW
+#define MSEG_SPEC_HSW 8
+#endif
+constexpr int SPEC_HSW = MSEG_SPEC_HSW;  // hot keys loaded together in a scan of a lane's LDS queue
+static_assert(SPEC_QCAP % SPEC_HSW == 0, "hot-key scans read whole groups of SPEC_HSW entries");
 static_assert(SPEC_NX == 4, "k_spec_round keeps SPEC_NX record chunk bases in four registers");
 
 __device__ __forceinline__ unsigned long long spec_claim(unsigned tag, int rank, unsigned popped) {
@@ -234,10 +239,12 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
   // pop, so a long cascade is cheaper as serial pops).  But a fallback restarts the rest of the
   // bucket as a new generation; where long cascades are everywhere (uniform noise at 4096^2:
   // invasion-percolation avalanches of thousands of pops) those re-runs and the regime's
-  // cooldowns cost far more than slow lanes, so after a fallback executions may run SPEC_MAXREC
-  // pops, until a generation's executions all stay within the short cap again
+  // cooldowns cost far more than slow lanes.  Default policy (capmode 7): the stable prefix's head
+  // (its inputs final, it runs once more at most) may always run SPEC_MAXREC pops; every execution
+  // from round 2 on may too once the flood is in deep mode (SpecCtl.deep: a cooldown after large
+  // generations).  Modes 0-5 are the round-4 A/B alternatives (MSEG_SPEC_CAPMODE)
   const int capmode = ws.spec_capmode;
-  const bool lcap = capmode == 7 ? ctl->spec.deep != 0 : ctl->spec.longcap != 0;
+  const bool lcap = capmode == 7 ? ctl->spec.deep == 1 : ctl->spec.longcap != 0;
   const int par = (int)(T & 1u), ppar = (int)((T - 1u) & 1u);
   // replays need complete change marks: no overflowing execution (claims never logged in full)
   // below the item in the last two rounds
@@ -479,15 +486,23 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
           cold_add(k);
           return;
         }
+        // one pass: where the largest hot key is, and the largest of the others (keys are unique)
         int mi = 0;
+        unsigned long long h2 = k;
         #pragma unroll 1
-        for (int e = 1; e < SPEC_QCAP; ++e)
-          if (lq[e * SPEC_BS + tid] == hmx) mi = e;
+        for (int k0 = 0; k0 < SPEC_QCAP; k0 += SPEC_HSW) {
+          unsigned long long e[SPEC_HSW];
+  #pragma unroll
+          for (int i = 0; i < SPEC_HSW; ++i) e[i] = lq[(k0 + i) * SPEC_BS + tid];
+  #pragma unroll
+          for (int i = 0; i < SPEC_HSW; ++i) {
+            if (e[i] == hmx) mi = k0 + i;
+            else h2 = max(h2, e[i]);
+          }
+        }
         cold_add(hmx);
         lq[mi * SPEC_BS + tid] = k;
-        hmx = k;
-        #pragma unroll 1
-        for (int e = 0; e < SPEC_QCAP; ++e) hmx = max(hmx, lq[e * SPEC_BS + tid]);
+        hmx = h2;
       };
       // hot empty, cold not: the SPEC_QCAP smallest cold keys become hot (one pass keeping the
       // smallest seen, one pass compacting the rest in place)
@@ -514,12 +529,16 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
               lq[hmi * SPEC_BS + tid] = v[k];
               hmax = 0;
               #pragma unroll 1
-              for (int e = 0; e < SPEC_QCAP; ++e) {
-                const unsigned long long u = lq[e * SPEC_BS + tid];
-                if (u > hmax) {
-                  hmax = u;
-                  hmi = e;
-                }
+              for (int e0 = 0; e0 < SPEC_QCAP; e0 += SPEC_HSW) {
+                unsigned long long u[SPEC_HSW];
+  #pragma unroll
+                for (int i = 0; i < SPEC_HSW; ++i) u[i] = lq[(e0 + i) * SPEC_BS + tid];
+  #pragma unroll
+                for (int i = 0; i < SPEC_HSW; ++i)
+                  if (u[i] > hmax) {
+                    hmax = u[i];
+                    hmi = e0 + i;
+                  }
               }
             }
           }
@@ -592,14 +611,20 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
       // next pop: the smallest key (lowest level, oldest push) of the lane's queue
       auto select = [&]() -> int {
         if (nq == 0) refill();
+        // SPEC_HSW hot keys per LDS round trip (loads past nq read dead entries, ignored)
         int bi = 0;
-        unsigned long long be = lq[tid];
-        for (int k = 1; k < nq; ++k) {
-          const unsigned long long e = lq[k * SPEC_BS + tid];
-          if (e < be) {
-            be = e;
-            bi = k;
-          }
+        unsigned long long be = ~0ull;
+        #pragma unroll 1
+        for (int k0 = 0; k0 < nq; k0 += SPEC_HSW) {
+          unsigned long long e[SPEC_HSW];
+  #pragma unroll
+          for (int i = 0; i < SPEC_HSW; ++i) e[i] = lq[(k0 + i) * SPEC_BS + tid];
+  #pragma unroll
+          for (int i = 0; i < SPEC_HSW; ++i)
+            if (k0 + i < nq && e[i] < be) {
+              be = e[i];
+              bi = k0 + i;
+            }
         }
         --nq;
         lq[bi * SPEC_BS + tid] = lq[nq * SPEC_BS + tid];
@@ -973,11 +998,12 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
         s.block = 0;
       }
       if (!s.fallback && s.xmax <= 0) s.longcap = 0;  // every execution within the short cap
-      // judged slower than serial pops: long final cascades serialised one per round as heads of
-      // the stable prefix (uniform noise at 4096^2: invasion-percolation avalanches everywhere).
+      // judged slower than serial pops: maybe long final cascades serialised one per round as heads
+      // of the stable prefix (uniform noise at 4096^2: invasion-percolation avalanches everywhere).
       // Besides the cooldown, from here on every execution may run long from round 2 on
-      // (SpecCtl.deep; round 4 A/B: 16.7 -> 1.6 s there, neutral on album.jpg and random 1024^2)
-      if (slow) s.deep = 1;
+      // (SpecCtl.deep; round 4 A/B: 16.7 -> 1.66 s there).  Judged slow again in deep mode, the
+      // flood's generations are small ones that long executions only slow down (album.jpg): off
+      if (slow) s.deep = s.deep == 0 ? 1 : 2;
       if (slow) {
         s.on = 0;
         s.block = 0;

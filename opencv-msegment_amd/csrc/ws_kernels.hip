@@ -1836,12 +1836,12 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
   CF_STAMP(0);
   const Batch B = s_B;
   const int ncommit = s_ncommit, flags = s_flags;
-  unsigned* const arrive = &ctl->farrive.v[0];
+  Ctl::Arrive* const arrive = ctl->farrive;
   if ((int)blockIdx.x < G) {
     // ---- a sub-round block ----
     const int vb = blockIdx.x, ch = vb / SUBS, i0 = ch * CH + (vb % SUBS) * 1024;
     if (!(flags & 1) || i0 >= ncommit) {  // block-uniform: nothing to scatter, done reading
-      if (tid == 0) atomicAdd(&arrive[blockIdx.x & 7], 1u);
+      if (tid == 0) atomicAdd(&arrive[blockIdx.x & 7].v, 1u);
       return;
     }
     // Sub-rounds vb, vb + G, ... (up to FAST_PASS of them: batches of up to FAST_PASS * G / SUBS
@@ -1868,7 +1868,7 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
       ++npass;
     }
     // this block's reads of the control block and of the rows are complete
-    if (tid == 0) atomicAdd(&arrive[blockIdx.x & 7], 1u);
+    if (tid == 0) atomicAdd(&arrive[blockIdx.x & 7].v, 1u);
 #ifdef MSEG_CF_PROF
     if (cfd && tid == 0 && blockIdx.x == 0) atomicAdd(&cfd[6], (unsigned long long)((long long)__builtin_amdgcn_s_memrealtime() - cf_t0));
 #endif
@@ -2000,7 +2000,7 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
     const int expect = G;
     long long t0 = 0;
     for (;;) {
-      unsigned v = (tid < 8) ? __hip_atomic_load(&arrive[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      unsigned v = (tid < 8) ? __hip_atomic_load(&arrive[tid].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
 #pragma unroll
       for (int o = 4; o > 0; o >>= 1) v += __shfl_xor(v, o);
       v = __builtin_amdgcn_readlane(v, 0);
@@ -2013,7 +2013,7 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
         break;
       }
     }
-    if (tid < 8) arrive[tid] = 0u;  // every arrival is in: reset for the next launch
+    if (tid < 8) arrive[tid].v = 0u;  // every arrival is in: reset for the next launch
     CF_STAMP(3);
   }
   __syncthreads();

@@ -136,8 +136,8 @@ struct SpecCtl {
   int longcap;              // executions may run SPEC_MAXREC pops (else Ws.spec_maxrec): set by a
                             // fallback, cleared by a generation whose executions all stayed short
   int xmax;                 // longest execution (pops) of the current generation, all rounds
-  int deep;                 // sticky, set by the first cooldown: from round 2 on every execution
-                            // may run SPEC_MAXREC pops
+  int deep;                 // 1: from round 2 on every execution may run SPEC_MAXREC pops; set
+                            // by the flood's first cooldown, 2 (off for good) by a second one
   long long replays;        // executions whose cascade was replayed from the previous round
 };
 
@@ -196,13 +196,13 @@ struct Ctl {
   unsigned hold;     // epoch of a decided batch k_commit_fast declined (k_resolve must not re-run it)
   int pad3;
   // k_commit_fast: sub-round blocks done reading, by blockIdx % 8 (zeroed after): 480 atomics per
-  // launch and the finalizer's polls, on a line of their own (round 4: sharing one with the batch
-  // words every block reads at its start cost the headline ~4%)
+  // launch and the finalizer's polls, one 128-B line per counter (atomics on one line serialise at
+  // the L2: with all 8 counters on one line k_commit_fast took 14.8 us per launch, round 4)
   struct alignas(128) Arrive {
-    unsigned v[8];
-    unsigned pad[24];
+    unsigned v;
+    unsigned pad[31];
   };
-  Arrive farrive;
+  Arrive farrive[8];
   // k_spec_round's contended words, one 128-B line each: device-scope atomics on one line
   // serialise (~11 ns each), and a round issues thousands of them
   struct alignas(128) Hot {
