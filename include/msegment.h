@@ -182,8 +182,9 @@ int msg_set_batch_inflight(msg_ctx* ctx, int k);
 int msg_set_batch_floods(msg_ctx* ctx, int mode);
 
 /* Blocks per launch of the flood's decision kernel (0 = default: one wave of the device's
- * occupancy).  A performance knob only: its rank chunks are dealt in dispatch order, so any
- * grid size -- and any number of concurrent floods -- makes progress. */
+ * occupancy, halved for each flood of a batch call with two or more floods in flight).  A
+ * performance knob only: its rank chunks are dealt in dispatch order, so any grid size -- and
+ * any number of concurrent floods -- makes progress. */
 int msg_set_resolve_grid(msg_ctx* ctx, int blocks);
 
 /* ---- device-resident entry points (dense layouts; pointers are device memory of the

@@ -80,6 +80,7 @@ struct msg_ctx {
   unsigned epoch = 1;
   int group = 8;
   int res_grid = 0;   // k_resolve blocks per launch (occupancy x CUs by default; a perf knob)
+  bool res_grid_set = false;  // msg_set_resolve_grid chose it (batches then keep it as it is)
   int commit_subs = FAST_SUBS;  // k_commit_fast sub-round blocks: the whole chip, or a share of it
                                 // per flood when a batch keeps several in flight (run_batch)
   msg_stats stats{};
@@ -752,7 +753,9 @@ int run_batch(msg_ctx* c, int n, F fn) {
   }
   for (int w = 0; w < k; ++w) {
     c->subs[w]->commit_subs = csubs;
-    c->subs[w]->res_grid = c->res_grid;
+    // ... and, unless msg_set_resolve_grid chose one, half the default k_resolve grid (8 frames of
+    // 4096^2, 4 in flight: 8833 -> 9230 Mpx/s, profiles/r04o_batch_grid_probe.log)
+    c->subs[w]->res_grid = (c->res_grid_set || k < 2) ? c->res_grid : std::max(c->cus, c->res_grid / 2);
     c->subs[w]->spec = c->spec;
     c->subs[w]->fast = c->fast;
     c->subs[w]->serk = c->serk;
@@ -1503,6 +1506,7 @@ int msg_watershed_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size
 
 int msg_set_resolve_grid(msg_ctx* c, int blocks) {
   if (!c || blocks < 0) return MSG_EINVAL;
+  c->res_grid_set = blocks > 0;
   if (blocks == 0) {
     int per = 0;
     HIPCHK(c, hipSetDevice(c->dev));

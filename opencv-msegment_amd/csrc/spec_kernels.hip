@@ -854,6 +854,7 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
   const unsigned long long etag = (unsigned long long)ctl->bat.epoch << 32;
   __shared__ int s_tile, s_off, s_tot;
   __shared__ int wsum[SPEC_FT / 64];
+  __shared__ int s_ex[SPEC_FT], s_bx[SPEC_FT];  // the tile's items: first virtual rank, log base
   if (P == 0) {  // nothing final (overflow at rank 0): the batch engine takes the bucket's head
     if (blockIdx.x == 0 && tid == 0) {
       s.longcap = 1;
@@ -907,6 +908,8 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
       if (k < wv) excl += wsum[k];
       tot += wsum[k];
     }
+    s_ex[tid] = excl;
+    s_bx[tid] = rc.x;
     if (tid == 0) {
       int prev = 0;
       if (tile > 0) {
@@ -931,12 +934,17 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
       s_tot = prev + tot;
     }
     __syncthreads();
-    const int v0 = s_off + excl;
-    for (int k = 0; k < rc.y; ++k) {
-      const unsigned long long r = ws.slog[rc.x + k];
+    // the tile's records, dealt over the whole block (an item's records used to be one thread's
+    // loop: a long execution's thousands of records held the commit for milliseconds)
+    for (int q = tid; q < tot; q += SPEC_FT) {
+      int lo = 0;  // the last item whose first virtual rank is <= q (empty items share the next's)
+#pragma unroll
+      for (int h = SPEC_FT / 2; h > 0; h >>= 1)
+        if (s_ex[lo + h] <= q) lo += h;
+      const unsigned long long r = ws.slog[s_bx[lo] + (q - s_ex[lo])];
       const int y = (int)(r & 0x0fffffffu);
       const unsigned dm = (unsigned)(r >> 28) & 15u;
-      const int v = v0 + k;
+      const int v = s_off + q;
       const unsigned wy = (unsigned)ws.w4[y];
       ws.ipx[v] = y;
       ws.tl[v] = etag | (uint32_t)(r >> 32);
