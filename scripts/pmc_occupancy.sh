@@ -11,7 +11,9 @@ i=0
 for g in "${CGROUPS[@]}"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $g --output-format csv -d "$OUT/g$i" -o run -- \
-      python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile-pass --batch-frames 0 > "$OUT/g$i.log" 2>&1
+      python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile-pass --batch-frames 0 --stress-steps 0 --no-hwq4 --many-frames 0 > "$OUT/g$i.log" 2>&1
   rc=$?; echo "group $i rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done
+# the per-dispatch counter files are large: keep the per-kernel table only
+python scripts/pmc_table.py "$OUT" "$OUT/table.json" > "$OUT/table.txt" 2>&1 && rm -rf "$OUT"/g[0-9]*/

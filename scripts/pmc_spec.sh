@@ -17,3 +17,4 @@ for g in "${CGROUPS[@]}"; do
   [ $rc -eq 0 ] || exit $rc
 done
 python scripts/pmc_table.py $OUT $OUT/pmc_table.json > $OUT/pmc_table.txt 2>&1
+rm -rf "$OUT"/g[0-9]*/
