@@ -125,6 +125,23 @@ __device__ __forceinline__ SpecRec spec_load(const Ws& ws, const SpecView& V, in
   return r;
 }
 
+// The same record for the top pop's gather, before the item writes anything this round: plain
+// loads (L1-cacheable, two 16-B loads).  A line cached before another wave's write of this round
+// only hides words spec_decide ignores or reads equivalently: other items' round-T claims and
+// labels are not used for a non-own view, and a final claim promoted this round equals that
+// item's round T - 1 claim, which the view then takes instead.
+__device__ __forceinline__ SpecRec spec_load_pre(const Ws& ws, const SpecView& V, int z) {
+  const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(&V.spx[z].cl[0]);
+  const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(&V.spx[z].fin);
+  SpecRec r;
+  r.cl0 = a.x;
+  r.cl1 = a.y;
+  r.fin = b.x;
+  r.labs = b.y;
+  r.s = ws.mk[z];
+  return r;
+}
+
 // State of pixel z as item j sees it: > 0 label, WSHED, 0 unknown, INQ queued or pushed.
 // Own writes first, then final items' writes, then the previous round's lower ranks, else the
 // pre-generation state.
@@ -186,9 +203,16 @@ __device__ __forceinline__ bool spec_replay_clean(const Ws& ws, int base, int nr
 // End of a round (last block): grow the stable prefix, or hand the generation to the commit.
 __device__ void spec_finalize(Ctl* ctl, int P, int n, unsigned T, unsigned G, unsigned long long* dg) {
   SpecCtl& s = ctl->spec;
-  if (dg) {  // diagnostics: sum over rounds of the round's longest wave
-    dg[5] += __hip_atomic_load(&s.rmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (dg) {  // diagnostics: sums over rounds of the round's longest wave and of its split
+    const unsigned long long k = __hip_atomic_load(&s.rmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    dg[5] += k >> 40;              // its lifetime
+    dg[4] += (k >> 20) & 0xfffffu; // its waits for earlier items' top pops
+    dg[6] += k & 0xfffffu;         // its top-pop writes + cascades
+    const unsigned long long k2 = __hip_atomic_load(&s.rmax2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    dg[0] += (k2 >> 20) & 0xfffffu;  // its dealing + promotion of final items' claims
+    dg[1] += k2 & 0xfffffu;          // its log copy, change marks, candidates
     s.rmax = 0;
+    s.rmax2 = 0;
   }
   // written by this kernel's atomics: read at L2, not through a line cached at kernel start
   const int fc = __hip_atomic_load(&ctl->sfc.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -266,10 +290,10 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
 #endif
   unsigned long long* const dg = ws.diag ? ws.diag + 8 : nullptr;  // msg_set_diag: the round's wall-clock split (10 ns ticks)
   const long long tk0 = dg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
-  long long tw = 0, tc = 0;
-  int maxrec = 0;
+  long long tw = 0, tc = 0, tpr = 0, tpo = 0;  // diag: waits, cascades, dealing + promotion, post
   __syncthreads();
   while (!stop) {
+    const long long tq0 = dg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
     int r0 = 0;
     // (pre-checking the word with a load before the atomic, sharding the log counter per
     // blockIdx % 8 and skipping rank-minimum atomics already beaten measured 26% slower)
@@ -292,6 +316,7 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
           if ((dm >> d) & 1u) st_ag64(&ws.spx[nbi(y + marg, d, Wt) - marg].fin, fin_word(G, 0u, 0));
       }
     }
+    if (dg) tpr += (long long)__builtin_amdgcn_s_memrealtime() - tq0;
     // ---- execute [P, n): gather the top pop ----
     const bool ex = j >= P && j < n;
     int p = 0;
@@ -310,7 +335,13 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
       for (int d = 0; d < 4; ++d) nbp[d] = nbi(pb, d, Wt) - marg;
       SpecRec rr[4];  // all four records in flight before the first decision
 #pragma unroll
-      for (int d = 0; d < 4; ++d) rr[d] = spec_load(ws, V, nbp[d]);
+      for (int d = 0; d < 4; ++d) {
+#ifdef MSEG_SPEC_GATHER_AG  // A/B: the gather through agent-scope loads too (round-4 baseline)
+        rr[d] = spec_load(ws, V, nbp[d]);
+#else
+        rr[d] = spec_load_pre(ws, V, nbp[d]);
+#endif
+      }
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         if (rr[d].s <= -3) {  // an earlier item of this generation: its top pop of this round
@@ -745,7 +776,7 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
     if (dg) {
       tw += tkb - tka;
       tc += (long long)__builtin_amdgcn_s_memrealtime() - tkb;
-      maxrec = max(maxrec, nrec);
+      tpo -= (long long)__builtin_amdgcn_s_memrealtime();  // + the chunk's end below
     }
     {  // the generation's longest execution (SpecCtl.longcap)
       const int wx = -wave_min(ex ? -nrec : 0);
@@ -801,20 +832,20 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
       const int nex = max(0, min(n, r0 + 64) - max(P, r0));
       if (nex) atomicAdd(&s_exec, nex);
     }
+    if (dg) tpo += (long long)__builtin_amdgcn_s_memrealtime();
   }
   if (dg) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) maxrec = max(maxrec, __shfl_xor(maxrec, o));
     if (lane == 0) {
       const long long tot = (long long)__builtin_amdgcn_s_memrealtime() - tk0;
-      atomicAdd(&dg[0], (unsigned long long)tw);  // wave time in the top-pop waits
-      atomicAdd(&dg[1], (unsigned long long)tc);  // wave time in top-pop writes + cascades
       atomicAdd(&dg[2], (unsigned long long)tot); // wave time in the kernel
       atomicMax(&dg[3], (unsigned long long)tot); // longest wave
-      atomicMax(&dg[4], (unsigned long long)maxrec);
-      atomicMax(&dg[6], (unsigned long long)tc);
       atomicAdd(&dg[7], 1ull);
-      atomicMax(&ctl->spec.rmax, (unsigned long long)tot);
+      // the round's longest wave with its wait / cascade split (10 ns ticks, 20 bits each)
+      atomicMax(&ctl->spec.rmax, ((unsigned long long)tot << 40) | ((unsigned long long)min(tw, 0xfffffll) << 20) |
+                                     (unsigned long long)min(tc, 0xfffffll));
+      // ... and its dealing + promotion / post-execution split (the same wave unless two tie)
+      atomicMax(&ctl->spec.rmax2, ((unsigned long long)tot << 40) | ((unsigned long long)min(tpr, 0xfffffll) << 20) |
+                                      (unsigned long long)min(tpo, 0xfffffll));
     }
   }
 #ifdef MSEG_SPEC_PROF

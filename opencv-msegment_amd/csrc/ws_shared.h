@@ -131,7 +131,8 @@ struct SpecCtl {
   long long tspec, pspec;    // since the regime start: generations' own time (+ a commit estimate
                              // each) and the pops they committed -- what the regime is judged on
   long long gens, rounds_total, execs, cpops, fallbacks;
-  unsigned long long rmax;  // diagnostics: longest wave of this round (10 ns ticks)
+  unsigned long long rmax;  // diagnostics: longest wave of this round (10 ns ticks) | waits | cascades
+  unsigned long long rmax2; // ... | its dealing + promotion | its post-execution work
   int ov1, ov2;             // lowest overflowing rank of the last / the one-before-last round
   int longcap;              // executions may run SPEC_MAXREC pops (else Ws.spec_maxrec): set by a
                             // fallback, cleared by a generation whose executions all stayed short

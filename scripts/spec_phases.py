@@ -55,10 +55,11 @@ def main():
         seg.set_diag(False)
         d = st["diag"]
         w = max(1, d[7])
-        print("%s: flood %.1f ms (diag on) | waves %d, per wave: waits %.1f us, cascades %.1f us, kernel %.1f us |"
-              " sum of longest waves %.1f ms over %d rounds (%.1f us/round) | longest cascade %.1f us, most records %d" % (
-                  nm, t0.elapsed_time(t1), d[7], d[0] / w / 100, d[1] / w / 100, d[2] / w / 100, d[5] / 1e5,
-                  st["spec_rounds"], d[5] / 100 / max(1, st["spec_rounds"]), d[6] / 100, d[4]), flush=True)
+        print("%s: flood %.1f ms (diag on) | waves %d, %.1f us each | sum of the rounds' longest waves %.1f ms over"
+              " %d rounds (%.1f us/round): dealing + promotion %.1f ms, top-pop waits %.1f ms, top-pop writes +"
+              " cascades %.1f ms, log copy + change marks %.1f ms" % (
+                  nm, t0.elapsed_time(t1), d[7], d[2] / w / 100, d[5] / 1e5, st["spec_rounds"],
+                  d[5] / 100 / max(1, st["spec_rounds"]), d[0] / 1e5, d[4] / 1e5, d[6] / 1e5, d[1] / 1e5), flush=True)
     seg.close()
 
 
