@@ -1,5 +1,6 @@
 # round 4: deep-mode A/B -- MSEG_SPEC_DEEPREC (cap of non-head executions in deep mode) and
 # MSEG_SPEC_DEEPCOOL=0 (no cooldown on entering deep mode), regime probe per setting
+# (both knobs were removed after this A/B: profiles/r04v_ab_deep_mode.log)
 set -u
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r04v; mkdir -p $O
