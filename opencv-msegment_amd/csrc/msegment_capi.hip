@@ -465,13 +465,15 @@ int flood_begin(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int H,
   ws.qcap = c->qcap;
 
   // speculative generations: tiled indices must fit their 28-bit log field.  The engine's
-  // workspace (~64 B/px) is allocated lazily: only once a flood of this context has entered the
-  // interrupt-dense (serial-pop) regime, which k_scan reports through the progress mirror; smooth
-  // frames never pay for it.  From then on it is kept (msg_set_speculative(ctx, 0) frees it).
+  // workspace (~64 B/px) is allocated up front for frames of 2^20 tiled pixels or more, lazily
+  // for smaller ones (once a flood of this context has entered the interrupt-dense regime, which
+  // k_scan reports through the progress mirror).  Round 4: allocated in the middle of a flood,
+  // the first flood of a context on uniform noise at 4096^2 took 16.2 s (the later ones 1.45 s;
+  // scripts/first_flood.py).  From then on it is kept (msg_set_speculative(ctx, 0) frees it).
   fr.ntiled = (long long)((H + 3) / 4) * ws.Wt * 16;
   fr.spec = c->spec && !multi && fr.ntiled <= (1ll << 28) && H >= 3 && W >= 3;
   fr.spec_bound = false;
-  if (fr.spec && c->spec_np > 0) {  // allocated by an earlier flood: (re)size and arm it now
+  if (fr.spec && (c->spec_np > 0 || fr.ntiled >= (1ll << 20))) {  // (re)size and arm it now
     rc = ensure_spec(c, fr.ntiled, N, st);
     if (rc) return rc;
     fr.spec_bound = true;
