@@ -62,10 +62,11 @@ typedef struct msg_stats {
     int64_t diag[8];        /* msg_set_diag counters (0 when off): k_resolve gather cycles,
                                dependency-loop cycles, loop rounds, max loop cycles, wave-rounds;
                                small-batch loop rounds, small-batch loop entries; reserved.
-                               When speculative generations ran: wave time in top-pop waits,
-                               in cascades, in the round kernel (10 ns ticks), longest wave,
-                               most records of an execution, longest wait, longest cascade,
-                               waves                                                            */
+                               When speculative generations ran (10 ns ticks): sums over the
+                               rounds of the round's longest wave's dealing + promotion and of
+                               its log copy + change marks; wave time in the round kernel;
+                               longest wave; sums over the rounds of the longest wave's top-pop
+                               waits, of its whole time, of its top-pop writes + cascades; waves */
     /* speculative generations (the interrupt-dense regime; msg_set_speculative) */
     int64_t spec_generations;   /* generations committed                                        */
     int64_t spec_rounds;        /* rounds run (every generation needs >= 2: run + confirm)      */
