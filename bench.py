@@ -17,7 +17,13 @@ N > 1 (launched by torch.distributed.run, one rank per GPU): every rank segments
 collectives are the timing barriers and the max-over-ranks of the elapsed time.
 
 Rank 0 prints ONE JSON line.  Extra objects: "roofline" (dominant kernel, HIP-event timed on the
-launch stream), "cpu_baseline" (the C oracle = same algorithm, timed on this host, rank 0, N=1).
+launch stream), "cpu_baseline" (the C oracle = same algorithm, timed on this host, rank 0, N=1),
+and side lines that are parity cases, not the headline: "batch" (BASELINE config 5 per GPU: 8
+frames per call, digest-checked), "stress" / "stress_random" (config 3's mosaic+noise and uniform
+random variants, digest-checked, 1-core oracle beside them), "many_floods" (1024
+notConnectedMarkers floods of 1024^2 per call in the many-floods mode, every frame checked
+against the oracle, 16-thread oracle beside it; --many-frames), "colour_distance" (the stand-alone
+L-inf stencil against the HBM roofline).
 """
 import argparse
 import hashlib
