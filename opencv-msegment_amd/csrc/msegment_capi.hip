@@ -1139,12 +1139,18 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
     // depend on how many of the blocks are resident (msg_set_resolve_grid overrides it)
     c->res_grid = cus * std::max(1, std::min(per, 4));
     c->cus = cus;
-    // k_spec_round: as many blocks as fit at once (LDS cascade queues, VGPRs); ranks are dealt
-    // in dispatch order, so this is a performance choice only
+    // k_spec_round: one block per CU (two fit; ranks are dealt in dispatch order, so this is a
+    // performance choice only).  Round 4 A/B (profiles/r04sg_ab_spec_grid.log, flood only):
+    // 2 -> 1 block per CU took mosaic+noise 1024^2 47.4 -> 35.9 ms, 4096^2 186.6 -> 175.2 ms,
+    // uniform noise 4096^2 1444 -> 1424 ms, album.jpg 1313 -> 1300 ms (fewer waves contending for
+    // the dealing counter and the L2 at every round's start and end); half a block per CU was
+    // better still on the 1024^2 frames and worse at 4096^2
     int sper = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&sper, k_spec_round, SPEC_BS, 0) != hipSuccess || sper <= 0)
       sper = 1;
-    c->spec_grid = cus * sper;
+    c->spec_grid = cus * std::min(sper, 1);
+    if (const char* e = getenv("MSEG_SPEC_GRID"))  // A/B knob: k_spec_round blocks (at most one wave of them)
+      c->spec_grid = std::max(1, std::min(atoi(e), cus * sper));
   }
   *out = c;
   return MSG_OK;
