@@ -55,15 +55,17 @@ BYTES_PER_PIXEL = {"k_prep": 15.0, "k_untile": 11.0, "k_colorize": 7.0, "k_edge_
                    "k_gray_hist": 4.0, "k_nc_markers": 5.0,
                    # shape marker stage: 1 B in + 1 B out per pixel for the 8-bit stencils
                    "k_gray": 4.0, "k_median": 2.0, "k_canny_nms": 2.0, "k_ring_median3": 2.0}
-# k_resolve per item: queue entry 4 + own weights 4 + 4 neighbour states 16, out ipx 4 + granule 8
-# + desc 8 (push-competitor reads are data dependent and not counted)
-BYTES_PER_ITEM = {"k_resolve": 44.0}        # per batch item resolved
-# k_spec_round per pop it executes, top pops and cascade pops alike: queue entry 4 + own weights 4
-# + 4 neighbour states 16 in, claim 8 + label 4 + record 8 out.  Executed pops = the executions
-# (top pops) + the cascade pops they ran = executions x (pops per committed execution), i.e.
-# spec_executions * spec_gen_pops / committed executions; the engine counts committed pops, so the
-# per-round cascade pops are estimated from the committed ratio (round 3 left them out).
-BYTES_PER_EXEC = {"k_spec_round": 44.0}
+# Per-unit algorithmic bytes of the flood kernels whose unit is not a pixel, each over the units
+# that kernel itself processed (msg_stats counts them where the work happens, so no kernel is
+# priced on another's units -- round 4's stress lines priced k_resolve on every committed virtual
+# item of the speculative engine and printed frac 1.19):
+# k_resolve per item of the batches it decided (msg_stats.resolve_items): queue entry 4 + own
+# weights 4 + 4 neighbour states 16 in, out ipx 4 + granule 8 + desc 8 (push-competitor reads are
+# data dependent and not counted).
+# k_spec_round per pop it ran pop by pop (msg_stats.spec_exec_pops: top pops and cascade pops of
+# the executions that were not replayed, every round): queue entry 4 + own weights 4 + 4 neighbour
+# states 16 in, claim 8 + label 4 + record 8 out (replayed executions' log reads are not counted).
+BYTES_PER_UNIT = {"k_resolve": (44.0, "resolve_items"), "k_spec_round": (44.0, "spec_exec_pops")}
 # k_scatter and k_commit_fast: per committed item 24 B (descriptor 8 + pixel 4 + granule 8 in,
 # state 4 out), per appended push 8 B (queue slot 4 + state 4 out); each over the items that path
 # committed (msg_stats fast_* / scatter_*)
@@ -145,13 +147,9 @@ def kernel_roofline(prof, stats_per_step, npx, steps):
             continue
         if name in BYTES_PER_PIXEL:
             alg = BYTES_PER_PIXEL[name] * npx * steps
-        elif name in BYTES_PER_ITEM:
-            alg = BYTES_PER_ITEM[name] * stats_per_step["items"] * steps
-        elif name in BYTES_PER_EXEC:
-            ex = stats_per_step["spec_executions"]
-            gens_items = max(1, stats_per_step["spec_gen_pops"] - stats_per_step["spec_cascade_pops"])
-            pops_per_exec = stats_per_step["spec_gen_pops"] / gens_items  # 1 + cascade pops per item
-            alg = BYTES_PER_EXEC[name] * ex * pops_per_exec * steps or None
+        elif name in BYTES_PER_UNIT:
+            per, unit = BYTES_PER_UNIT[name]
+            alg = per * stats_per_step[unit] * steps or None
         elif name == "k_scatter":
             alg = (BYTES_SCATTER[0] * stats_per_step["scatter_pops"]
                    + BYTES_SCATTER[1] * stats_per_step["scatter_pushes"]) * steps or None
@@ -310,26 +308,15 @@ def batch_hwq4(args, S, seed):
     2, 3 and 4 floods in flight."""
     import subprocess
 
-    out = None
-    for prio in ("", "high"):  # the default stream priority, then high-priority context streams
-        env = dict(os.environ, MSEG_BENCH_HWQ="4")
-        env.pop("MSEG_STREAM_PRIORITY", None)
-        if prio:
-            env["MSEG_STREAM_PRIORITY"] = prio
-        cmd = [sys.executable, os.path.abspath(__file__), "--batch-only", "--size", str(S), "--kind", args.kind,
-               "--seed", str(seed), "--batch-frames", str(args.batch_frames)]
-        try:
-            r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
-            line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
-            res = json.loads(line)
-        except Exception as e:  # noqa: BLE001 -- reported, not fatal to the headline line
-            res = {"error": "batch_hwq4 child failed: %s" % e}
-        res["stream_priority"] = prio or "default"
-        if out is None:
-            out = res
-        else:
-            out["alt_" + (prio or "default")] = res
-    return out
+    env = dict(os.environ, MSEG_BENCH_HWQ="4")
+    cmd = [sys.executable, os.path.abspath(__file__), "--batch-only", "--size", str(S), "--kind", args.kind,
+           "--seed", str(seed), "--batch-frames", str(args.batch_frames)]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+        line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+        return json.loads(line)
+    except Exception as e:  # noqa: BLE001 -- reported, not fatal to the headline line
+        return {"error": "batch_hwq4 child failed: %s" % e}
 
 
 def batch_only(args):
@@ -470,11 +457,22 @@ def stress_line(seg, S, sync, dev, steps, cpu=True, kind="mosaic_noise", seed=2)
 
     from msegment import synth
 
+    import msegment
+
     img, m, depth = synth.frame(kind, S, S, seed)
     t_img = torch.from_numpy(img).to(dev)
     t_m = torch.from_numpy(m).to(dev)
     t_lab = torch.empty_like(t_m)
     t_dst = torch.empty((S, S, 3), dtype=torch.uint8, device=dev)
+    # the first flood of a fresh context (workspace allocation included), timed on its own: the
+    # timed steps below reuse the bench context, so a first-flood cliff would not show in them
+    sync()
+    t0 = time.perf_counter()
+    fresh = msegment.Segmenter(dev.index)
+    fresh.watershed_colorize_dev(t_img, t_m, t_lab, depth, None, t_dst)
+    sync()
+    first_ms = 1000.0 * (time.perf_counter() - t0)
+    fresh.close()
     seg.watershed_colorize_dev(t_img, t_m, t_lab, depth, None, t_dst)
     sync()
     st = seg.stats()
@@ -494,7 +492,9 @@ def stress_line(seg, S, sync, dev, steps, cpu=True, kind="mosaic_noise", seed=2)
     out = {"workload": "%s %dx%d seed %d, watershed + colorByIndexes(colored=false), device-resident "
                        "(BASELINE config 3 stress variant)" % (kind, S, S, seed),
            "value": round(value, 3), "unit": "Mpx/s", "steps": steps,
-           "ms_per_step": round(1000.0 * dt / steps, 3), "parity": parity}
+           "ms_per_step": round(1000.0 * dt / steps, 3), "parity": parity,
+           "first_flood_ms": round(first_ms, 3),
+           "first_flood_note": "one step on a freshly created context (its workspace allocation included)"}
     # the dominant kernel of the same step, HIP-event timed (one profiled step); the flood's
     # counters from that step (the first flood of a context may run part of the way without the
     # speculative engine, which is allocated on first use)

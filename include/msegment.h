@@ -48,7 +48,7 @@ extern "C" {
 #define MSG_ERANGE   (-6)  /* output array too small / search space beyond what the
                               reference could finish (documented per entry point)          */
 
-#define MSG_ABI_VERSION 5
+#define MSG_ABI_VERSION 6
 
 typedef struct msg_ctx msg_ctx;
 
@@ -85,9 +85,13 @@ typedef struct msg_stats {
     int64_t fast_pops, fast_pushes;        /* committed / appended by k_commit_fast             */
     int64_t scatter_pops, scatter_pushes;  /* committed / appended through k_scan + k_scatter
                                               (batches above 4096 items, phase 1, generations) */
+    /* the other priced kernels' units, counted where the work happens */
+    int64_t resolve_items;      /* items of the batches k_resolve decided (its re-runs included) */
+    int64_t spec_exec_pops;     /* pops k_spec_round ran pop by pop: the top pops and cascade pops
+                                   of every execution that was not replayed, over all rounds     */
 } msg_stats;
 
-#define MSG_NKERNELS 25
+#define MSG_NKERNELS 24
 typedef struct msg_kernel_profile {
     char    name[32];       /* kernel name, e.g. "k_resolve"                                   */
     int64_t launches;       /* launches timed since the last reset                              */
@@ -120,8 +124,8 @@ int  msg_get_kernel_profile(msg_ctx* ctx, msg_kernel_profile* out, int max_entri
  * enable == 2 also injects faults for tests: the decision kernel's odd blocks give up their
  * first chunk of every batch once, which exercises the give-up / re-run path.
  * enable == 3 reports the regime split instead: tiny batches, their pops, their time
- * (s_memrealtime, 10 ns ticks); serial pops, their time; k_serial launches that popped, their
- * LDS line fills; pops of small batches (65..4096 items). */
+ * (s_memrealtime, 10 ns ticks); serial pops, their time; two reserved counters; pops of small
+ * batches (65..4096 items). */
 int  msg_set_diag(msg_ctx* ctx, int enable);
 /* Speculative generations for the interrupt-dense regime (textured frames, scattered seeds):
  * on by default.  enable = 0 keeps the batch engine's serial pops there instead (A/B runs and
@@ -131,12 +135,6 @@ int  msg_set_speculative(msg_ctx* ctx, int enable);
  * the next batch) instead of three (decide, one-block scan, scatter): on by default; 0 keeps
  * the three-launch iterations (A/B runs and tests).  Results are identical either way. */
 int  msg_set_fast_commit(msg_ctx* ctx, int enable);
-/* The serial-pop regime (interrupt-dense floods: real photographs, scattered seeds) in a kernel of
- * its own (k_serial: one wave, queue bookkeeping in registers and LDS records, stores deferred
- * behind the next pop's loads) instead of inside the one-workgroup batch loop.  Off by default:
- * ~1.03 us per pop against the in-loop pops' slightly faster flood times (DESIGN.md section 7,
- * scripts/serial_phases.py for its per-pop split).  Results are identical either way. */
-int  msg_set_serial_kernel(msg_ctx* ctx, int enable);
 
 /* ---- host-buffer entry points (synchronous; strides in BYTES) ---------------------------- */
 
@@ -179,7 +177,9 @@ int msg_set_batch_inflight(msg_ctx* ctx, int k);
  *   mode 1: every flood popped serially to its end in that kernel;
  *   mode 2: a flood that pops 4096 times in a row without pushing below its level (a plateau,
  *           where batches pay) is finished by the full engine instead.
- * Results are identical in every mode (each is cv::watershed's exact serial order). */
+ * Results are identical in every mode (each is cv::watershed's exact serial order).
+ * Memory: the per-frame workspaces stay allocated on the context between calls (the next call of
+ * the same size reuses them) until mode 0 is set again, which releases them, or msg_destroy. */
 int msg_set_batch_floods(msg_ctx* ctx, int mode);
 
 /* Blocks per launch of the flood's decision kernel (0 = default: one wave of the device's

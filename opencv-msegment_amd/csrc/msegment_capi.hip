@@ -49,16 +49,12 @@ struct msg_ctx {
   long long qcap = 0;
   // speculative generations (spec_kernels.hip): allocated on the first flood that may use them
   bool fast = true;             // msg_set_fast_commit: two-launch iterations for large batches
-  bool serk = false;            // msg_set_serial_kernel: serial pops in k_serial (one wave, register queue state)
   bool spec = true;             // msg_set_speculative
   long long spec_np = 0, spec_logcap = 0;
   SpecPx* d_spx = nullptr;       // per tiled pixel: both parities' claims and labels, final claim
   unsigned long long *d_stl = nullptr, *d_slog = nullptr;
   unsigned long long *d_ssig = nullptr, *d_stmp = nullptr, *d_sflag = nullptr, *d_sxp = nullptr;
   long long spec_xcap = 0;       // d_sxp entries (k_spec_round's per-round chunk pool)
-  int spec_maxrec = SPEC_MAXREC_SHORT;  // pops per execution before it overflows while no recent
-                                       // generation fell back (MSEG_SPEC_MAXREC overrides)
-  int spec_capmode = 7;          // MSEG_SPEC_CAPMODE (A/B): see k_spec_round
   int4* d_srec = nullptr;
   int2* d_sfrec = nullptr;
   unsigned* d_sdirt = nullptr;
@@ -142,7 +138,7 @@ namespace {
 enum KernelId { KID_PREP, KID_INIT_SCAN, KID_COMPACT, KID_RESOLVE, KID_SCAN, KID_SCATTER,
                 KID_COLORIZE, KID_EDGE, KID_UNTILE, KID_GRAY_HIST, KID_NC_MARKERS, KID_SPEC_ROUND,
                 KID_GRAY, KID_MEDIAN, KID_CANNY, KID_CCL, KID_RING, KID_NUMBER, KID_HOLES, KID_SPEC_FLATTEN,
-                KID_COLOR, KID_BILATERAL, KID_COMMIT_FAST, KID_SERIAL, KID_SERIAL_MULTI };
+                KID_COLOR, KID_BILATERAL, KID_COMMIT_FAST, KID_SERIAL_MULTI };
 const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_compact", "k_resolve",
                                                 "k_scan", "k_scatter", "k_colorize",
                                                 "k_edge_weights", "k_untile", "k_gray_hist",
@@ -150,7 +146,7 @@ const char* const kKernelNames[MSG_NKERNELS] = {"k_prep", "k_init_scan", "k_comp
                                                 "k_median", "k_canny_nms", "k_ccl", "k_ring_median3",
                                                 "k_cc_number", "k_holes", "k_spec_flatten",
                                                 "k_color_stage", "k_bilateral", "k_commit_fast",
-                                                "k_serial", "k_serial_multi"};
+                                                "k_serial_multi"};
 
 hipEvent_t pool_event(msg_ctx* c) {
   if (c->evused == c->evpool.size()) {
@@ -403,8 +399,6 @@ void bind_spec(msg_ctx* c, FloodRun& fr, bool on) {
   ws.sdirt = on ? c->d_sdirt : nullptr;
   ws.sxp = on ? c->d_sxp : nullptr;
   ws.sxcap = on ? std::min<long long>(c->spec_xcap, 0x7fffffffll) : 0;
-  ws.spec_maxrec = c->spec_maxrec;
-  ws.spec_capmode = c->spec_capmode;
   ws.snp = on ? c->spec_np : 0;
   ws.slogcap = on ? c->spec_logcap : 0;
   ws.spec_lazy = (fr.spec && !on) ? 1 : 0;
@@ -425,6 +419,7 @@ int flood_begin(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int H,
   fr.W = W;
   fr.N = N;
   fr.st = st;
+  fr.ws = Ws{};  // a zero-pixel flood keeps ctl == nullptr: k_serial_multi skips it
   if (N == 0) return MSG_OK;
   int rc = ensure_flood(c, H, W, st);
   if (rc) return rc;
@@ -455,7 +450,6 @@ int flood_begin(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int H,
   ws.diag = c->diag ? c->d_diag : nullptr;
 
   ws.hmir = c->d_mir;
-  ws.serk = c->serk ? 1 : 0;
   ws.multi = multi ? 1 : 0;
   ws.H = H;
   ws.W = W;
@@ -516,9 +510,7 @@ int flood_loop(msg_ctx* c, FloodRun& fr) {
   c->h_mir[4] = 0;
   c->h_mir[5] = 0;
   c->h_mir[6] = 0;
-  c->h_mir[7] = 0;
   int it = 0, prev_end = -1;
-  bool ser_seen = false;
   c->group = 4;
   long long syncs = 0;
   // Two kinds of iteration, chosen per group from the regime the last poll reported (a stale
@@ -531,16 +523,7 @@ int flood_loop(msg_ctx* c, FloodRun& fr) {
     const bool spec_it = fr.spec_bound && c->h_mir[4] != 0;
     // two-launch iterations while the last report was a large flood batch (k_commit_fast)
     const bool fast_it = !spec_it && c->fast && c->h_mir[6] != 0;
-    const bool ser_it = !spec_it && c->serk && c->h_mir[7] != 0;
-    // once this flood has entered the serial regime, every three-launch iteration ends with a
-    // k_serial (a no-op unless that iteration's k_scan handed the regime over), so the hand-over
-    // does not wait for the host to see it
-    ser_seen = ser_seen || (c->serk && c->h_mir[7] != 0);
     for (int g = 0; g < c->group; ++g, ++it) {
-      if (ser_it) {  // serial pops pending: k_serial, one wave
-        LAUNCH(c, KID_SERIAL, st, k_serial, dim3(1), dim3(64), 0, ws, it);
-        continue;
-      }
       if (fast_it) {
         if (c->inject)  // test only: give-ups (msg_set_diag 2) -> k_commit_fast schedules re-runs
           LAUNCH(c, KID_RESOLVE, st, k_resolve<true>, dim3(gres), dim3(RBS), 0, ws);
@@ -565,7 +548,6 @@ int flood_loop(msg_ctx* c, FloodRun& fr) {
       }
       LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);  // + small batches
       LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, it);
-      if (ser_seen) LAUNCH(c, KID_SERIAL, st, k_serial, dim3(1), dim3(64), 0, ws, it);
     }
     HIPCHK(c, hipGetLastError());
     if (prev_end >= 0) {
@@ -629,6 +611,8 @@ int flood_end(msg_ctx* c, FloodRun& fr, int32_t* d_labels, int depth = 0, const 
   c->stats.fast_pushes = std::max(0ll, tail.pushes - tail.spushes - tail.lpushes);
   c->stats.scatter_pops = tail.spops;
   c->stats.scatter_pushes = tail.spushes;
+  c->stats.resolve_items = tail.ritems;
+  c->stats.spec_exec_pops = tail.spec.xpops;
   // when speculative generations ran, diag reports their round split instead (spec_kernels.hip)
   for (int k = 0; k < 8; ++k)
 #ifdef MSEG_CF_PROF
@@ -703,6 +687,17 @@ int upload_palette(msg_ctx* c, const uint8_t* pal, int depth, hipStream_t st) {
 
 constexpr int MAX_INFLIGHT = 8;
 
+// Batch totals: every counter of msg_stats summed over the frames (diag included), the frame size
+// of the last one.
+void add_stats(msg_stats& tot, const msg_stats& s) {
+  static_assert(sizeof(msg_stats) % sizeof(int64_t) == 0, "msg_stats is int64 fields only");
+  int64_t* t = reinterpret_cast<int64_t*>(&tot);
+  const int64_t* a = reinterpret_cast<const int64_t*>(&s);
+  for (size_t k = 0; k < sizeof(msg_stats) / sizeof(int64_t); ++k) t[k] += a[k];
+  tot.rows = s.rows;
+  tot.cols = s.cols;
+}
+
 int ensure_subs(msg_ctx* c, int k) {
   while ((int)c->subs.size() < k) {
     msg_ctx* sub = nullptr;
@@ -720,15 +715,7 @@ template <class F>
 int run_batch(msg_ctx* c, int n, F fn) {
   const int k = std::max(1, std::min({c->inflight, n, MAX_INFLIGHT}));
   msg_stats tot{};
-  auto add = [&tot](const msg_stats& s) {
-    tot.batches += s.batches;
-    tot.pops += s.pops;
-    tot.host_syncs += s.host_syncs;
-    tot.items += s.items;
-    tot.pushes += s.pushes;
-    tot.rows = s.rows;
-    tot.cols = s.cols;
-  };
+  auto add = [&tot](const msg_stats& s) { add_stats(tot, s); };
   if (k == 1) {
     for (int i = 0; i < n; ++i) {
       const int rc = fn(i, c);
@@ -747,12 +734,8 @@ int run_batch(msg_ctx* c, int n, F fn) {
   // k in flight: each flood's commit grid takes a 1/k share of the chip (its blocks then take up
   // to FAST_PASS sub-rounds each), so that concurrent floods' commits overlap instead of each
   // filling every wave slot; at least FAST_SUBS / FAST_PASS blocks (the batches reported as
-  // fitting FAST_CH chunks still fit).  MSEG_BATCH_COMMIT_SUBS overrides (A/B runs).
-  int csubs = std::max(FAST_SUBS / FAST_PASS, (FAST_SUBS / k) / (CH / 1024) * (CH / 1024));
-  if (const char* e = getenv("MSEG_BATCH_COMMIT_SUBS")) {
-    const int v = atoi(e);
-    if (v > 0) csubs = std::max(FAST_SUBS / FAST_PASS, std::min(FAST_SUBS, v / (CH / 1024) * (CH / 1024)));
-  }
+  // fitting FAST_CH chunks still fit).
+  const int csubs = std::max(FAST_SUBS / FAST_PASS, (FAST_SUBS / k) / (CH / 1024) * (CH / 1024));
   for (int w = 0; w < k; ++w) {
     c->subs[w]->commit_subs = csubs;
     // ... and, unless msg_set_resolve_grid chose one, half the default k_resolve grid (8 frames of
@@ -760,7 +743,6 @@ int run_batch(msg_ctx* c, int n, F fn) {
     c->subs[w]->res_grid = (c->res_grid_set || k < 2) ? c->res_grid : std::max(c->cus, c->res_grid / 2);
     c->subs[w]->spec = c->spec;
     c->subs[w]->fast = c->fast;
-    c->subs[w]->serk = c->serk;
     if (c->subs[w]->diag != c->diag || c->subs[w]->inject != c->inject) {
       rc = msg_set_diag(c->subs[w], c->inject ? 2 : c->diag ? 1 : 0);
       if (rc) return rc;
@@ -783,13 +765,7 @@ int run_batch(msg_ctx* c, int n, F fn) {
           rcs[w] = r;
           return;
         }
-        acc.batches += sub->stats.batches;
-        acc.pops += sub->stats.pops;
-        acc.host_syncs += sub->stats.host_syncs;
-        acc.items += sub->stats.items;
-        acc.pushes += sub->stats.pushes;
-        acc.rows = sub->stats.rows;
-        acc.cols = sub->stats.cols;
+        add_stats(acc, sub->stats);
       }
       if (hipStreamSynchronize(sub->own) != hipSuccess) rcs[w] = MSG_EHIP;
       st[w] = acc;
@@ -846,7 +822,6 @@ int batch_many(msg_ctx* c, int n, int depth, const uint8_t* d_pal, F frame) {
     msg_ctx* x = c->msubs[k];
     x->res_grid = c->res_grid;
     x->fast = c->fast;
-    x->serk = false;
     x->spec = false;  // the full engine finishes handed-back floods without the speculative engine
     const uint8_t* img;
     const int32_t* mk;
@@ -913,13 +888,7 @@ int batch_many(msg_ctx* c, int n, int depth, const uint8_t* d_pal, F frame) {
           rcs[w] = r;
           return;
         }
-        acc.batches += x->stats.batches;
-        acc.pops += x->stats.pops;
-        acc.host_syncs += x->stats.host_syncs;
-        acc.items += x->stats.items;
-        acc.pushes += x->stats.pushes;
-        acc.rows = x->stats.rows;
-        acc.cols = x->stats.cols;
+        add_stats(acc, x->stats);
       }
       st[w] = acc;
     });
@@ -933,13 +902,7 @@ int batch_many(msg_ctx* c, int n, int depth, const uint8_t* d_pal, F frame) {
         if (!c->msubs[k]->err.empty()) c->err = c->msubs[k]->err;
       return rcs[w];
     }
-    tot.batches += st[w].batches;
-    tot.pops += st[w].pops;
-    tot.host_syncs += st[w].host_syncs;
-    tot.items += st[w].items;
-    tot.pushes += st[w].pushes;
-    tot.rows = st[w].rows;
-    tot.cols = st[w].cols;
+    add_stats(tot, st[w]);
   }
   c->stats = tot;
   return MSG_OK;
@@ -1097,12 +1060,8 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
   msg_ctx* c = new (std::nothrow) msg_ctx();
   if (!c) return MSG_ENOMEM;
   c->dev = device_ordinal;
-  if (const char* e = getenv("MSEG_SPEC_MAXREC"))  // A/B knob: the execution length cap
-    c->spec_maxrec = std::max(1, std::min(atoi(e), SPEC_MAXREC));
-  if (const char* e = getenv("MSEG_SPEC_CAPMODE"))  // A/B knob: when the long cap applies
-    c->spec_capmode = atoi(e);
-  // MSEG_STREAM_PRIORITY=high|low: the context's stream at that priority (a tuning knob for
-  // concurrent floods: the HIP runtime keeps streams of different priorities on different
+  // MSG_CREATE_HIGH_PRIORITY: the context's stream at the device's highest priority (the batch
+  // entry points' sub-contexts: the HIP runtime keeps streams of different priorities on different
   // hardware queues)
   int prio = 0;
   if (hipSetDevice(c->dev) != hipSuccess) {  // the priority range below is the current device's
@@ -1110,10 +1069,8 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
     return MSG_EHIP;
   }
   {
-    const char* e = getenv("MSEG_STREAM_PRIORITY");
     int lo = 0, hi = 0;
-    if ((e || (flags & MSG_CREATE_HIGH_PRIORITY)) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
-      prio = (e && e[0] == 'l') ? lo : (e && e[0] == 'd') ? 0 : hi;
+    if ((flags & MSG_CREATE_HIGH_PRIORITY) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) prio = hi;
   }
   if (hipSetDevice(c->dev) != hipSuccess ||
       hipStreamCreateWithPriority(&c->own, hipStreamNonBlocking, prio) != hipSuccess ||
@@ -1149,8 +1106,6 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&sper, k_spec_round, SPEC_BS, 0) != hipSuccess || sper <= 0)
       sper = 1;
     c->spec_grid = cus * std::min(sper, 1);
-    if (const char* e = getenv("MSEG_SPEC_GRID"))  // A/B knob: k_spec_round blocks (at most one wave of them)
-      c->spec_grid = std::max(1, std::min(atoi(e), cus * sper));
   }
   *out = c;
   return MSG_OK;
@@ -1206,13 +1161,6 @@ int msg_set_fast_commit(msg_ctx* c, int enable) {
   if (!c) return MSG_EINVAL;
   c->fast = enable != 0;
   for (msg_ctx* sub : c->subs) sub->fast = c->fast;
-  return MSG_OK;
-}
-
-int msg_set_serial_kernel(msg_ctx* c, int enable) {
-  if (!c) return MSG_EINVAL;
-  c->serk = enable != 0;
-  for (msg_ctx* sub : c->subs) sub->serk = c->serk;
   return MSG_OK;
 }
 
@@ -1567,6 +1515,15 @@ int msg_watershed_colorize_batch_dev(msg_ctx* c, int n, const void* const* d_bgr
 int msg_set_batch_floods(msg_ctx* c, int mode) {
   if (!c || mode < 0 || mode > 2) return MSG_EINVAL;
   c->many = mode;
+  if (mode == 0) {  // the mode's per-frame workspaces (~44 B/px each) are released with it
+    if (hipSetDevice(c->dev) != hipSuccess) return fail(c, MSG_EHIP, "hipSetDevice failed");
+    for (msg_ctx* sub : c->msubs) msg_destroy(sub);
+    c->msubs.clear();
+    dfree(c->d_wss);
+    c->wss_cap = 0;
+    dfree(c->d_mstage);
+    c->mstage_cap = 0;
+  }
   return MSG_OK;
 }
 

@@ -42,17 +42,9 @@
 namespace msg {
 
 constexpr unsigned SPEC_RMAX = (1u << 22) - 1;
-#ifndef MSEG_SPEC_MINB
-#define MSEG_SPEC_MINB 2  // two blocks per CU (the LDS allows two): caps the registers at 256
-#endif
-#ifndef MSEG_SPEC_RFW
-#define MSEG_SPEC_RFW 8
-#endif
-constexpr int SPEC_RFW = MSEG_SPEC_RFW;  // cold keys loaded together in a refill pass
-#ifndef MSEG_SPEC_HSW
-#define MSEG_SPEC_HSW 8
-#endif
-constexpr int SPEC_HSW = MSEG_SPEC_HSW;  // hot keys loaded together in a scan of a lane's LDS queue
+constexpr int SPEC_MINB = 2;  // blocks per CU the register budget allows (the LDS allows two)
+constexpr int SPEC_RFW = 8;   // cold keys loaded together in a refill pass
+constexpr int SPEC_HSW = 8;   // hot keys loaded together in a scan of a lane's LDS queue
 static_assert(SPEC_QCAP % SPEC_HSW == 0, "hot-key scans read whole groups of SPEC_HSW entries");
 static_assert(SPEC_NX == 4, "k_spec_round keeps SPEC_NX record chunk bases in four registers");
 
@@ -250,30 +242,29 @@ __device__ void spec_finalize(Ctl* ctl, int P, int n, unsigned T, unsigned G, un
 
 // One round.  Waves take 64 consecutive ranks at a time from [Pold, n) in dispatch order:
 // [Pold, P) promote their claims, [P, n) execute.
-__global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
+__global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
   Ctl* ctl = ws.ctl;
   if (ctl->bat.mode != 3 || ctl->spec.state != 1 || ctl->error) return;
   __shared__ unsigned long long lq[SPEC_QCAP * SPEC_BS];  // per-lane cascade queues, [entry][lane]
-  __shared__ int s_exec, s_rep;
+  __shared__ int s_exec, s_rep, s_xpop;
   const int tid = threadIdx.x, lane = lane_id();
-  if (tid == 0) s_exec = s_rep = 0;
+  if (tid == 0) s_exec = s_rep = s_xpop = 0;
   const unsigned T = ctl->spec.T, G = ctl->spec.G;
   const int P = ctl->spec.P, n = ctl->spec.n, L = ctl->spec.L, bstart = ctl->spec.bstart;
-  // An execution may run ws.spec_maxrec pops (a lane's cascade pop costs several times a serial
-  // pop, so a long cascade is cheaper as serial pops).  But a fallback restarts the rest of the
-  // bucket as a new generation; where long cascades are everywhere (uniform noise at 4096^2:
+  // An execution may run SPEC_MAXREC_SHORT pops (a lane's cascade pop costs several times a
+  // serial pop, so a long cascade is cheaper as serial pops).  But a fallback restarts the rest of
+  // the bucket as a new generation; where long cascades are everywhere (uniform noise at 4096^2:
   // invasion-percolation avalanches of thousands of pops) those re-runs and the regime's
-  // cooldowns cost far more than slow lanes.  Default policy (capmode 7): the stable prefix's head
-  // (its inputs final, it runs once more at most) may always run SPEC_MAXREC pops; every execution
-  // from round 2 on may too once the flood is in deep mode (SpecCtl.deep: a cooldown after large
-  // generations).  Modes 0-5 are the round-4 A/B alternatives (MSEG_SPEC_CAPMODE)
-  const int capmode = ws.spec_capmode;
-  const bool lcap = capmode == 7 ? ctl->spec.deep == 1 : ctl->spec.longcap != 0;
+  // cooldowns cost far more than slow lanes.  So the stable prefix's head (its inputs final, it
+  // runs once more at most) may always run SPEC_MAXREC pops, and every execution from round 2 on
+  // may too once the flood is in deep mode (SpecCtl.deep: a cooldown after large generations).
+  // Round 4 A/B'd six such policies (profiles/r04v_ab_deep_mode.log); this one won.
+  const bool lcap = ctl->spec.deep == 1;
   const int par = (int)(T & 1u), ppar = (int)((T - 1u) & 1u);
   // replays need complete change marks: no overflowing execution (claims never logged in full)
   // below the item in the last two rounds
   const int ovlim = min(ctl->spec.ov1, ctl->spec.ov2);
-  int nrep = 0;
+  int nrep = 0, nxpop = 0;  // this lane's replayed executions; pops it ran pop by pop
   SpecView V;
   V.spx = ws.spx;
   V.par = par;
@@ -336,11 +327,7 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
       SpecRec rr[4];  // all four records in flight before the first decision
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-#ifdef MSEG_SPEC_GATHER_AG  // A/B: the gather through agent-scope loads too (round-4 baseline)
-        rr[d] = spec_load(ws, V, nbp[d]);
-#else
         rr[d] = spec_load_pre(ws, V, nbp[d]);
-#endif
       }
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
@@ -477,20 +464,25 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
       // smallest live keys are "hot" in LDS; the rest are "cold" in a chunk of the round's pool,
       // every cold key larger than every hot one.
       int nq = 0, nc = 0;   // hot / cold keys
-      int cb = -1;          // cold chunk in ws.sxp
+      int cb = -1;          // cold chunk in ws.sxp (-2: the pool was full, never asked again)
       unsigned cmin = 256;  // lowest level among the cold keys
       unsigned long long hmx = 0;  // largest hot key (pops take the smallest: it stays valid)
       unsigned qseq = 0;    // pushes of this execution
+      // a chunk of sz entries of the round's pool, or -1 once it is full.  The counter is only
+      // bumped while it is below the pool's size, so it stays far from 2^31 (at most one chunk per
+      // lane in flight past the end), and a negative offset is refused regardless
       auto pool_get = [&](int sz) -> int {
+        if (ld_ag32(&ctl->sxtop.v) >= ws.sxcap) return -1;
         const int b = atomicAdd(&ctl->sxtop.v, sz);
-        return ((long long)b + sz <= ws.sxcap) ? b : -1;
+        return (b >= 0 && (long long)b + sz <= ws.sxcap) ? b : -1;
       };
       auto cold_add = [&](unsigned long long k) {
-#ifdef MSEG_SPEC_NOSPILL
-        ovf = cap = true;
-        return;
-#endif
+        if (cb == -2) {
+          ovf = cap = true;
+          return;
+        }
         if (cb < 0 && (cb = pool_get(SPEC_CCAP)) < 0) {
+          cb = -2;
           ovf = cap = true;
           return;
         }
@@ -683,21 +675,15 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
       }
       if (py >= 0) issue_writes(0);
       while (more) {
-        // the execution length cap (policy: Ws.spec_capmode, an A/B knob)
-        const bool longok = capmode == 1 ? lcap : capmode == 2 ? (T > G) : capmode == 3 ? (j == P)
-                          : capmode == 4 ? (lcap && T > G) : capmode == 5 ? (T > G || j == P)
-                          : capmode == 7 ? (j == P || (lcap && T > G)) : false;
-        if (nrec >= (longok ? SPEC_MAXREC : ws.spec_maxrec)) {  // a long cascade: cheaper as serial pops
+        // the execution length cap (see lcap above)
+        const bool longok = j == P || (lcap && T > G);
+        if (nrec >= (longok ? SPEC_MAXREC : SPEC_MAXREC_SHORT)) {  // a long cascade: cheaper as serial pops
           ovf = cap = true;
           break;
         }
         if (nrec >= SPEC_RL && (nrec - SPEC_RL) % SPEC_XCH == 0) {  // the next record starts a chunk
           const int c = (nrec - SPEC_RL) / SPEC_XCH;
-#ifdef MSEG_SPEC_NOSPILL
-          const int b = -1;
-#else
           const int b = c < SPEC_NX ? pool_get(SPEC_XCH) : -1;
-#endif
           if (b < 0) {
             ovf = cap = true;
             break;
@@ -778,10 +764,6 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
       tc += (long long)__builtin_amdgcn_s_memrealtime() - tkb;
       tpo -= (long long)__builtin_amdgcn_s_memrealtime();  // + the chunk's end below
     }
-    {  // the generation's longest execution (SpecCtl.longcap)
-      const int wx = -wave_min(ex ? -nrec : 0);
-      if (lane == 0 && wx > ws.spec_maxrec) atomicMax(&ctl->spec.xmax, wx);
-    }
     // ---- log space for the wave's records (one atomic per wave), signatures, change words ----
     const int want = (ex && !ovf && rbase < 0) ? nrec : 0;
     const int incl = wave_scan_add(want);
@@ -806,6 +788,7 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
       if (changed) fcand = j;
       if (ovf) ocand = j;
       if (rbase >= 0) ++nrep;
+      else nxpop += nrec;
       if (changed) {  // mark both executions' claims: round T + 1 replays nothing that viewed them
         unsigned* const dn = ws.sdirt + (size_t)par * ws.snp;
         auto mark = [&](unsigned long long r) {
@@ -858,10 +841,13 @@ __global__ __launch_bounds__(SPEC_BS, MSEG_SPEC_MINB) void k_spec_round(Ws ws) {
   }
 #endif
   if (nrep) atomicAdd(&s_rep, nrep);
+  nxpop = wave_sum(nxpop);
+  if (lane == 0 && nxpop) atomicAdd(&s_xpop, nxpop);
   __syncthreads();
   if (tid == 0) {
     atomicAdd((unsigned long long*)&ctl->spec.execs, (unsigned long long)s_exec);
     if (s_rep) atomicAdd((unsigned long long*)&ctl->spec.replays, (unsigned long long)s_rep);
+    if (s_xpop) atomicAdd((unsigned long long*)&ctl->spec.xpops, (unsigned long long)s_xpop);
     __threadfence();
     if (atomicAdd(&ctl->spec.ticket, 1) == (int)gridDim.x - 1) {
       __threadfence();
@@ -888,7 +874,6 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
   __shared__ int s_ex[SPEC_FT], s_bx[SPEC_FT];  // the tile's items: first virtual rank, log base
   if (P == 0) {  // nothing final (overflow at rank 0): the batch engine takes the bucket's head
     if (blockIdx.x == 0 && tid == 0) {
-      s.longcap = 1;
       Batch nb = ctl->bat;
       nb.mode = 0;
       nb.n = min(s.n, WMIN);
@@ -1030,13 +1015,11 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
         s.on = 0;
         s.block = slow ? 0 : L;
         s.fallbacks += 1;
-        s.longcap = 1;
         ctl->wcap = WMIN;
       } else if (Vn == P && s.n >= SPEC_QUIET) {  // a large generation without a cascade: batches pay
         s.on = 0;
         s.block = 0;
       }
-      if (!s.fallback && s.xmax <= 0) s.longcap = 0;  // every execution within the short cap
       // judged slower than serial pops: maybe long final cascades serialised one per round as heads
       // of the stable prefix (uniform noise at 4096^2: invasion-percolation avalanches everywhere).
       // Besides the cooldown, from here on every execution may run long from round 2 on

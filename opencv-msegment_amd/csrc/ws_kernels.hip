@@ -832,7 +832,6 @@ __device__ void spec_begin(Ctl* ctl, Batch& nb, int L, int bstart, int navail) {
   s.ticket = 0;
   ctl->slogtop.v = 0;
   ctl->sxtop.v = 0;
-  s.xmax = 0;
   s.fallback = 0;
   s.ftile = 0;
   s.tgen = (long long)__builtin_amdgcn_s_memrealtime();
@@ -1212,7 +1211,10 @@ __global__ __launch_bounds__(RBS, 4) void k_resolve(Ws ws) {
   __shared__ int s_skip[2], s_yield;
   __shared__ unsigned long long s_ctag;  // this run's chunk claims: {epoch, re-run}
   if (tid == 0) s_ctag = etag | (unsigned)B.rrun;
-  if (work && blockIdx.x == 0 && tid == 0) ctl->rsv = B.epoch;  // k_scan commits only decided batches
+  if (work && blockIdx.x == 0 && tid == 0) {
+    ctl->rsv = B.epoch;  // k_scan commits only decided batches
+    ctl->ritems += B.n;  // one writer per launch (block 0); re-runs count again: they redo the work
+  }
   if (tid == 0) s_yield = 0;
   for (int base = blockIdx.x * RBS; work && base < B.n; base += gridDim.x * RBS) {
     const int chunk = base / RBS;
@@ -1485,7 +1487,7 @@ __device__ Batch scan_body(const Ws& ws) {
     }
     return none;
   }
-  if (B.mode == 3 || B.mode == 4 || (B.mode == 0 && ctl->rsv != B.epoch)) {
+  if (B.mode == 3 || (B.mode == 0 && ctl->rsv != B.epoch)) {
     // not decided yet: speculative rounds still running, or an iteration without k_resolve
     // (the host queued the other iteration kind): nothing to commit here
     __syncthreads();
@@ -1732,7 +1734,6 @@ __global__ __launch_bounds__(1024) void k_scatter(Ws ws, int iter) {
     __hip_atomic_store(ws.hmir + 4, ws.ctl->spec.on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 5, ws.ctl->spec_want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 6, fast_batch(ws.ctl->bat, ws.ctl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(ws.hmir + 7, ws.ctl->bat.mode == 4 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const Batch B = ws.ctl->cbat;
@@ -2088,7 +2089,6 @@ __device__ __forceinline__ void commit_fast_body(Ws ws, int iter) {
     __hip_atomic_store(ws.hmir + 4, ctl->spec.on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 5, ctl->spec_want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 6, fast_batch(nb, ctl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(ws.hmir + 7, nb.mode == 4 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -2153,14 +2153,8 @@ __device__ __forceinline__ bool attempt_item_slots(const Item& it, const int (&v
 // wave_rank on the queue state the small loop keeps in LDS (in-order LDS within one wave).
 // Returns when the next batch has more than 64 items, the flood is done, or on error.
 constexpr int TINY_MAX = 64;
-#ifndef MSEG_SERIAL_RUN
-#define MSEG_SERIAL_RUN 4096
-#endif
-#ifndef MSEG_SERIAL_SWITCH
-#define MSEG_SERIAL_SWITCH 16
-#endif
-constexpr int SERIAL_RUN = MSEG_SERIAL_RUN;    // serial_loop: clean pops after which batches pay again
-constexpr int SERIAL_SWITCH = MSEG_SERIAL_SWITCH;  // a tiny batch cut before this many items -> serial_loop
+constexpr int SERIAL_RUN = 4096;    // serial_loop: clean pops after which batches pay again
+constexpr int SERIAL_SWITCH = 16;   // a tiny batch cut before this many items -> serial_loop
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -2460,7 +2454,6 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
   __shared__ int s_specgo, s_specblk;  // hand the regime to the speculative engine; its resume level
   __shared__ int s_specool;            // regime entries to skip first (SpecCtl.cool)
   __shared__ int s_lazyx;              // leave the launch: the speculative engine is being allocated
-  __shared__ int s_serx;               // leave the launch: serial pops in k_serial (mode 4)
   __shared__ Batch s_B;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const int Wt = ws.Wt;
@@ -2471,7 +2464,6 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     s_ser = 0;
     s_specgo = 0;
     s_lazyx = 0;
-    s_serx = 0;
     s_specblk = ws.spx ? ctl->spec.block : -1;  // -1: engine off
     s_specool = ctl->spec.cool;
   }
@@ -2495,11 +2487,6 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
         long long c4[4] = {0, 0, 0, 0};
         if (s_ser && s_specblk >= 0 && s_specool <= 0 && lowest_bucket(s_head, s_tail, 0) >= s_specblk) {
           if (lane == 0) s_specgo = 1;  // interrupt-dense: speculative generations from here on
-        } else if (s_ser && ws.serk) {
-          // the serial-pop regime runs in k_serial (LDS-cached state, launched by the host when
-          // the progress mirror shows mode 4): hand the queue state over
-          if (ws.spec_lazy && lane == 0) ctl->spec_want = 1;  // the host allocates the engine
-          if (lane == 0) s_serx = 1;
         } else if (s_ser) {
           if (ws.spec_lazy && lane == 0) ctl->spec_want = 1;  // the host allocates the engine
           const unsigned long long t0 = ws.diag ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -2533,7 +2520,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
         }
       }
       __syncthreads();
-      if (s_specgo || s_lazyx || s_serx) break;
+      if (s_specgo || s_lazyx) break;
       continue;
     }
     for (int k = tid; k < B.n; k += 1024) s_lab[k] = 0;
@@ -2723,7 +2710,6 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
       ctl->spec.on = 1;
       ctl->spec.block = 0;
     }
-    if (s_serx) nb.mode = 4;  // serial pops pending: only k_serial acts on this batch
     ctl->bat = nb;
     ctl->wcap = s_wcap;
     ctl->spec.cool = s_specool;
@@ -2742,527 +2728,29 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_serial: the serial-pop regime (see serial_loop) as a kernel of its own, one wave, launched by
-// the host when the progress mirror reports a batch in mode 4 ("serial pops pending", set by
-// k_scan's small-batch loop where it used to pop serially itself).  The same scalar program as
-// serial_loop -- pop the oldest item of the lowest non-empty bucket, fold its labelled
-// neighbours, push its unknown ones in L,R,T,B order -- laid out for a lone wave's latencies:
-//   * bucket b's {head, tail, base, tail at entry} is one 16-B LDS record (one ds_read_b128), the
-//     non-empty buckets a 256-bit mask in scalar registers (the lowest non-empty bucket is a
-//     find-first-set), the popped bucket's next 64 queue slots one VGPR, and the pixels this
-//     launch pushed a 16-entry LDS ring per bucket (an interrupt cascade pops what it just pushed);
-//   * a pop's one dependent memory round trip is the load of its four neighbours' states and its
-//     weights.  vmcnt counts loads and stores in issue order, so a load issued after a store waits
-//     for that store's acknowledgement too: the previous pop's stores (its label, its pushes'
-//     states and queue slots) are therefore issued AFTER this pop's loads, and the values this
-//     pop loaded from addresses the previous pop wrote are patched in registers.  Every lane
-//     stores the same value to the same address (one request), so the wave's later loads see it.
-constexpr int SER_RING = 16;
-
-struct SerStat {
-  long long pops = 0, pushes = 0, fills = 0;  // fills: ser_run_w's window loads
-  unsigned long long tsel = 0, tld = 0, tpush = 0;  // MSEG_SER_PROF: s_memtime cycles per phase
-};
-// the previous pop's writes, not yet issued: the label of pixel pp, and its pushes by direction
-// d in mask m (pixel z[d] queued at slot qs[d], state word sv[d]); indexed by the unrolled
-// direction only, so the arrays stay in registers
-struct SerPend {
-  int pp = -1, lab = 0;
-  unsigned m = 0;
-  int z[4], qs[4], sv[4];
-};
-// every value the whole wave computes alike is moved to a scalar register, so the pop's control
-// flow is scalar (no exec-mask bookkeeping around uniform branches)
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ void ser_mark(unsigned long long& ne0, unsigned long long& ne1, unsigned long long& ne2,
-                                         unsigned long long& ne3, int b, bool on) {
-  const unsigned long long bit = 1ull << (b & 63);
-  const int k = b >> 6;
-  const unsigned long long m0 = k == 0 ? bit : 0ull, m1 = k == 1 ? bit : 0ull, m2 = k == 2 ? bit : 0ull,
-                           m3 = k == 3 ? bit : 0ull;
-  if (on) {
-    ne0 |= m0; ne1 |= m1; ne2 |= m2; ne3 |= m3;
-  } else {
-    ne0 &= ~m0; ne1 &= ~m1; ne2 &= ~m2; ne3 &= ~m3;
-  }
-}
-__device__ __forceinline__ unsigned long long ser_clock() {
-#ifdef MSEG_SER_PROF
-  return __builtin_amdgcn_s_memtime();
-#else
-  return 0;
-#endif
-}
-// issue the pending writes (mkb: margin-relative states; state t of a tiled pixel z is mkb[z + marg]).
-// Always nine stores, absent ones to a dummy word: vmcnt counts in issue order, and with a fixed
-// number of stores behind a pop's loads the compiler waits for the loads only (vmcnt(9 + ...)),
-// not for these stores -- with a data-dependent count it must assume none and wait for all.
-__device__ __forceinline__ void ser_flush(const Ws& ws, int* mkb, int* dummy, SerPend& P) {
-  *(P.pp >= 0 ? mkb + P.pp : dummy) = P.lab;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const bool on = (P.m >> k) & 1u;
-    *(on ? ws.qbuf + P.qs[k] : dummy) = P.z[k] - ws.marg;
-    *(on ? mkb + P.z[k] : dummy) = P.sv[k];
-  }
-  P.pp = -1;
-  P.m = 0u;
-}
-
-// The pop loop of k_serial; returns when the queue is empty, after SERIAL_RUN pops without an
-// interrupt (batches pay again), at the speculative engine's hand-back points, or on an error.
-// Bucket records and rings in LDS are written by lane 0 (LDS is in order within the wave).
-__device__ __forceinline__ void ser_run(const Ws& ws, int4* s_bk, int (*s_bring)[SER_RING], unsigned long long* ne,
-                                        int& err, SerStat& S, int spec_block, long long cool_lim,
-                                        int run_limit = SERIAL_RUN) {
-  const int lane = lane_id();
-  const int Wt = ws.Wt, marg = ws.marg;
-  int* const mkb = ws.mk - marg;
-  const unsigned* const w4b = (const unsigned*)(ws.w4 - marg);
-  unsigned long long ne0 = ne[0], ne1 = ne[1], ne2 = ne[2], ne3 = ne[3];
-  int ring = 0, ring_l = -1, ring_h0 = 0, ring_n = 0, run = 0;
-  int* const dummy = &ws.ctl->pad3;  // nobody reads it
-  SerPend P;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) P.z[k] = P.qs[k] = P.sv[k] = 0;
-  for (;;) {
-    const unsigned long long t0 = ser_clock();
-    const int lo = ne0 ? __builtin_ctzll(ne0) : ne1 ? 64 + __builtin_ctzll(ne1)
-                 : ne2 ? 128 + __builtin_ctzll(ne2) : ne3 ? 192 + __builtin_ctzll(ne3) : NQ;
-    if (lo >= NQ || run >= run_limit) break;
-    if (spec_block > 0 && lo >= spec_block) break;  // the cascade that stopped the speculative engine is done
-    if (S.pops >= cool_lim) break;                  // its cooldown is over
-    if (ws.spec_lazy && S.pops >= 4096) break;      // the engine is being allocated: let it take over
-    const int4 rec = s_bk[lo];
-    const int h = uni(rec.x), tl = uni(rec.y), qb = uni(rec.z), be = uni(rec.w);
-    int p;
-    if (h >= be && h >= tl - SER_RING) {  // pushed by this launch: its LDS ring
-      p = uni(s_bring[lo][h & (SER_RING - 1)]);
-    } else if (lo == ring_l && h >= ring_h0 && h < ring_h0 + ring_n) {
-      p = __builtin_amdgcn_readlane(ring, h - ring_h0);
-    } else {  // the bucket's next 64 slots, one load per lane, after the pending writes (their slots)
-      ser_flush(ws, mkb, dummy, P);
-      ring_l = lo;
-      ring_h0 = h;
-      ring_n = min(tl - h, 64);
-      ring = (lane < ring_n) ? __hip_atomic_load(ws.qbuf + qb + h + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                             : 0;
-      p = __builtin_amdgcn_readlane(ring, 0);
-    }
-    const unsigned long long t1 = ser_clock();
-    const int pb = p + marg;
-    int nv[4], st[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) nv[d] = nbi(pb, d, Wt);
-#pragma unroll
-    for (int d = 0; d < 4; ++d) st[d] = __hip_atomic_load(mkb + nv[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const unsigned w4r = w4b[pb];
-    // the previous pop's writes go out now, behind this pop's loads; what they change is patched below
-    SerPend Q = P;
-    ser_flush(ws, mkb, dummy, P);
-    const unsigned w4 = (unsigned)uni((int)w4r);
-    int lab = 0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      int v = uni(st[d]);
-      if (nv[d] == Q.pp) v = Q.lab;
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (((Q.m >> k) & 1u) && nv[d] == Q.z[k]) v = Q.sv[k];
-      st[d] = v;
-      if (v > 0) lab = fold_lab(lab, v);
-    }
-    if (lab == 0) {  // impossible for an exact queue
-      err |= ERR_STATE;
-      lab = WSHED;
-    }
-    P.pp = pb;
-    P.lab = lab;
-    if (lane == 0) s_bk[lo].x = h + 1;
-    ++S.pops;
-    const unsigned long long t2 = ser_clock();
-    bool lower = false, lo_left = h + 1 < tl;
-    if (lab != WSHED) {
-      // the push targets' bucket records, all in one round trip
-      int4 tr[4];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) tr[d] = s_bk[(w4 >> (8 * d)) & 255u];
-      unsigned pm = 0u;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        if (st[d] != 0) continue;
-        const int t = (int)((w4 >> (8 * d)) & 255u);
-        int tt = uni(tr[d].y);
-        // an earlier push of this pop into the same bucket advanced its tail
-#pragma unroll
-        for (int e = 0; e < d; ++e)
-          if (st[e] == 0 && (int)((w4 >> (8 * e)) & 255u) == t) ++tt;
-        const int dest = uni(tr[d].z) + tt;
-        if (dest < 0 || (long long)dest >= ws.qcap) {
-          err |= ERR_CAPACITY;
-          continue;
-        }
-        const int z = nv[d] - marg;
-        P.z[d] = nv[d];
-        P.qs[d] = dest;
-        P.sv[d] = queued_state(dest);
-        pm |= 1u << d;
-        if (lane == 0) {
-          s_bring[t][tt & (SER_RING - 1)] = z;
-          s_bk[t].y = tt + 1;
-        }
-        ser_mark(ne0, ne1, ne2, ne3, t, true);
-        ++S.pushes;
-        lower = lower || t < lo;
-        lo_left = lo_left || t == lo;
-      }
-      P.m = pm;
-    }
-    if (!lo_left) ser_mark(ne0, ne1, ne2, ne3, lo, false);
-    run = lower ? 0 : run + 1;
-#ifdef MSEG_SER_PROF
-    const unsigned long long t3 = ser_clock();
-    S.tsel += t1 - t0;
-    S.tld += t2 - t1;
-    S.tpush += t3 - t2;
-#else
-    (void)t0;
-    (void)t1;
-    (void)t2;
-#endif
-    if (err) break;
-  }
-  ser_flush(ws, mkb, dummy, P);
-}
-
-// ser_run_w: the same pop loop with the states and weights of a window of SER_WT x SER_WT tiles
-// (48 x 48 pixels) around the pops held in LDS.  cv::watershed's serial regime is local -- an
-// interrupt pops what the last pop pushed, a bucket's FIFO neighbours were pushed by neighbours
-// (scripts/exp/window_hits.c: 76% of album.jpg's pops and 65% of uniform noise's have their
-// neighbourhood in a 24 x 24 window around the last miss) -- so most pops read their four
-// neighbours and weights from LDS (one LDS round trip) instead of memory (one ~1 us round trip
-// for a lone wave).  Writes go through: to memory (every lane the same value, one request) and
-// to the window.  A pop whose neighbourhood leaves the window reloads it centred on the pop: one
-// round trip for the whole window (12 tile rows, each a contiguous run of states and of weights),
-// issued after this wave's earlier stores, so it reads what they wrote.  Bucket bookkeeping as in
-// ser_run; the popped bucket's record lives in scalar registers while the loop stays on it.
-constexpr int SER_WT = 12;  // window tiles per side (4 x 4 pixels each)
-#ifndef MSEG_SER_WINDOW
-#define MSEG_SER_WINDOW 0  // 1: k_serial / k_serial_multi pop with ser_run_w (measured slower, round 4)
-#endif
-__device__ __forceinline__ void ser_run_w(const Ws& ws, int4* s_bk, int (*s_bring)[SER_RING], unsigned long long* ne,
-                                          int& err, SerStat& S, int spec_block, long long cool_lim, int run_limit,
-                                          int* win_s, int* win_w) {
-  const int lane = lane_id();
-  const int Wt = ws.Wt, marg = ws.marg;
-  const int Ht = (ws.H + 3) >> 2;
-  int* const mkb = ws.mk - marg;
-  const int* const mkf = ws.mk;  // frame-relative tiled states / weights
-  const int* const w4f = ws.w4;
-  unsigned long long ne0 = ne[0], ne1 = ne[1], ne2 = ne[2], ne3 = ne[3];
-  int ring = 0, ring_l = -1, ring_h0 = 0, ring_n = 0, run = 0;
-  const double invWt = 1.0 / (double)Wt;
-  int wr0 = -1, wc0 = 0;  // window origin (tile row, tile col); wr0 < 0: none loaded yet
-  // the popped bucket's record {head, tail, base, tail at entry} in registers (cur < 0: none)
-  int cur = -1, ch = 0, ctl_ = 0, cqb = 0, cbe = 0;
-  for (;;) {
-    const unsigned long long t0 = ser_clock();
-    const int lo = ne0 ? __builtin_ctzll(ne0) : ne1 ? 64 + __builtin_ctzll(ne1)
-                 : ne2 ? 128 + __builtin_ctzll(ne2) : ne3 ? 192 + __builtin_ctzll(ne3) : NQ;
-    if (lo >= NQ || run >= run_limit) break;
-    if (spec_block > 0 && lo >= spec_block) break;  // the cascade that stopped the speculative engine is done
-    if (S.pops >= cool_lim) break;                  // its cooldown is over
-    if (ws.spec_lazy && S.pops >= 4096) break;      // the engine is being allocated: let it take over
-    if (lo != cur) {
-      if (cur >= 0 && lane == 0) s_bk[cur] = make_int4(ch, ctl_, cqb, cbe);
-      const int4 rec = s_bk[lo];
-      cur = lo;
-      ch = uni(rec.x);
-      ctl_ = uni(rec.y);
-      cqb = uni(rec.z);
-      cbe = uni(rec.w);
-    }
-    const int h = ch;
-    int p;
-    if (h >= cbe && h >= ctl_ - SER_RING) {  // pushed by this launch: its LDS ring
-      p = uni(s_bring[lo][h & (SER_RING - 1)]);
-    } else if (lo == ring_l && h >= ring_h0 && h < ring_h0 + ring_n) {
-      p = __builtin_amdgcn_readlane(ring, h - ring_h0);
-    } else {  // the bucket's next 64 slots, one load per lane
-      ring_l = lo;
-      ring_h0 = h;
-      ring_n = min(ctl_ - h, 64);
-      ring = (lane < ring_n) ? __hip_atomic_load(ws.qbuf + cqb + h + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                             : 0;
-      p = __builtin_amdgcn_readlane(ring, 0);
-    }
-    const unsigned long long t1 = ser_clock();
-    // p's tile; the window holds p's 3 x 3 tile neighbourhood (where it exists) or is reloaded
-    const int T = p >> 4;
-    int tr = (int)((double)T * invWt);
-    if (tr * Wt > T) --tr;
-    else if ((tr + 1) * Wt <= T) ++tr;
-    tr = uni(tr);
-    const int tc = T - tr * Wt;
-    const bool hit = wr0 >= 0 && tr - (tr > 0 ? 1 : 0) >= wr0 && tr + (tr + 1 < Ht ? 1 : 0) < wr0 + SER_WT &&
-                     tc - (tc > 0 ? 1 : 0) >= wc0 && tc + (tc + 1 < Wt ? 1 : 0) < wc0 + SER_WT;
-    if (!hit) {
-      wr0 = max(0, min(tr - SER_WT / 2, Ht - SER_WT));
-      wc0 = max(0, min(tc - SER_WT / 2, Wt - SER_WT));
-      const int nr = min(SER_WT, Ht - wr0), nc4 = min(SER_WT, Wt - wc0) * 4;  // int4 per window tile row
-      int4 vs[SER_WT], vw[SER_WT];
-#pragma unroll
-      for (int i = 0; i < SER_WT; ++i) {  // every row of both planes in flight together
-        const bool on = i < nr && lane < nc4;
-        const long long g = ((long long)(wr0 + i) * Wt + wc0) * 16 + 4 * lane;
-        vs[i] = on ? *reinterpret_cast<const int4*>(mkf + g) : make_int4(0, 0, 0, 0);
-        vw[i] = on ? *reinterpret_cast<const int4*>(w4f + g) : make_int4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < SER_WT; ++i) {
-        if (i < nr && lane < nc4) {
-          *reinterpret_cast<int4*>(win_s + (i * SER_WT * 16 + 4 * lane)) = vs[i];
-          *reinterpret_cast<int4*>(win_w + (i * SER_WT * 16 + 4 * lane)) = vw[i];
-        }
-      }
-      ++S.fills;
-    }
-    // p and its four neighbours in the window (the same tiled neighbour rule, window-wide rows)
-    const int wb = ((tr - wr0) * SER_WT + (tc - wc0)) * 16 + (p & 15);
-    int wn[4], st[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) wn[d] = nbi(wb, d, SER_WT);
-#pragma unroll
-    for (int d = 0; d < 4; ++d) st[d] = uni(win_s[wn[d]]);
-    const unsigned w4 = (unsigned)uni(win_w[wb]);
-    int lab = 0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-      if (st[d] > 0) lab = fold_lab(lab, st[d]);
-    if (lab == 0) {  // impossible for an exact queue
-      err |= ERR_STATE;
-      lab = WSHED;
-    }
-    const int pb = p + marg;
-    mkb[pb] = lab;
-    if (lane == 0) win_s[wb] = lab;
-    ch = h + 1;
-    ++S.pops;
-    const unsigned long long t2 = ser_clock();
-    bool lower = false, lo_left = h + 1 < ctl_;
-    if (lab != WSHED) {
-      // the push targets' bucket records, all in one LDS round trip (the popped bucket's is in
-      // registers)
-      int4 tr4[4];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) tr4[d] = s_bk[(w4 >> (8 * d)) & 255u];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        if (st[d] != 0) continue;
-        const int t = (int)((w4 >> (8 * d)) & 255u);
-        int tt = (t == cur) ? ctl_ : uni(tr4[d].y);
-        const int qbt = (t == cur) ? cqb : uni(tr4[d].z);
-        // an earlier push of this pop into the same bucket advanced its tail
-#pragma unroll
-        for (int e = 0; e < d; ++e)
-          if (st[e] == 0 && (int)((w4 >> (8 * e)) & 255u) == t && t != cur) ++tt;
-        const int dest = qbt + tt;
-        if (dest < 0 || (long long)dest >= ws.qcap) {
-          err |= ERR_CAPACITY;
-          continue;
-        }
-        const int nb = nbi(pb, d, Wt);
-        const int qs = queued_state(dest);
-        ws.qbuf[dest] = nb - marg;
-        mkb[nb] = qs;
-        if (lane == 0) {
-          win_s[wn[d]] = qs;
-          s_bring[t][tt & (SER_RING - 1)] = nb - marg;
-          if (t != cur) s_bk[t].y = tt + 1;
-        }
-        if (t == cur) ctl_ = tt + 1;
-        ser_mark(ne0, ne1, ne2, ne3, t, true);
-        ++S.pushes;
-        lower = lower || t < lo;
-        lo_left = lo_left || t == lo;
-      }
-    }
-    if (!lo_left) ser_mark(ne0, ne1, ne2, ne3, lo, false);
-    run = lower ? 0 : run + 1;
-#ifdef MSEG_SER_PROF
-    const unsigned long long t3 = ser_clock();
-    S.tsel += t1 - t0;
-    S.tld += t2 - t1;
-    S.tpush += t3 - t2;
-#else
-    (void)t0;
-    (void)t1;
-    (void)t2;
-#endif
-    if (err) break;
-  }
-  if (cur >= 0 && lane == 0) s_bk[cur] = make_int4(ch, ctl_, cqb, cbe);
-}
-
-__global__ __launch_bounds__(64) void k_serial(Ws ws, int iter) {
-  Ctl* ctl = ws.ctl;
-  __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ];
-  __shared__ int s_bring[NQ][SER_RING];    // the last SER_RING pixels pushed to each bucket
-  __shared__ Seg s_seg[NQ];
-  __shared__ int s_err, s_nseg, s_n, s_specool, s_specblk;
-  const int lane = lane_id();
-  const Batch B0 = ctl->bat;
-  if (B0.mode == 4 && !ctl->error) {
-    __shared__ int4 s_bk[NQ];  // {head, tail, base, tail at entry} per bucket
-    __shared__ unsigned long long s_ne[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int b = 64 * k + lane;
-      const int hd = ctl->qhead[b], tl = ctl->qtail[b];
-      s_qbase[b] = ctl->qbase[b];
-      s_bk[b] = make_int4(hd, tl, s_qbase[b], tl);
-      const unsigned long long m = __ballot(tl > hd);
-      if (lane == 0) s_ne[k] = m;
-    }
-    if (lane == 0) {
-      s_specblk = ws.spx ? ctl->spec.block : -1;  // -1: engine off
-      s_specool = ctl->spec.cool;
-    }
-    wave_sync();
-    const int spec_block = s_specblk > 0 ? s_specblk : 0;
-    const long long cool_lim = (s_specblk >= 0 && s_specool > 0) ? s_specool : (1ll << 62);
-    const unsigned long long t_start = ws.diag ? __builtin_amdgcn_s_memrealtime() : 0;
-    const unsigned long long c_start = ser_clock();
-    SerStat S;
-    int err = 0;
-#if MSEG_SER_WINDOW
-    __shared__ int s_win[2][SER_WT * SER_WT * 16];
-    ser_run_w(ws, s_bk, s_bring, s_ne, err, S, spec_block, cool_lim, SERIAL_RUN, s_win[0], s_win[1]);
-#else
-    ser_run(ws, s_bk, s_bring, s_ne, err, S, spec_block, cool_lim);
-#endif
-    wave_sync();
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int4 r = s_bk[64 * k + lane];
-      s_head[64 * k + lane] = r.x;
-      s_tail[64 * k + lane] = r.y;
-    }
-    if (lane == 0) s_err = err;
-    const long long pops = S.pops, pushes = S.pushes;
-    if (ws.diag && lane == 0) {
-      atomicAdd(&ws.diag[19], (unsigned long long)pops);
-      atomicAdd(&ws.diag[20], __builtin_amdgcn_s_memrealtime() - t_start);
-      atomicAdd(&ws.diag[21], 1ull);
-#ifdef MSEG_SER_PROF  // the per-pop phase split (scripts/serial_phases.py), in shader cycles
-      atomicAdd(&ws.diag[16], S.tsel);
-      atomicAdd(&ws.diag[17], S.tld);
-      atomicAdd(&ws.diag[18], S.tpush);
-      atomicAdd(&ws.diag[22], ser_clock() - c_start);
-#else
-      (void)c_start;
-      atomicAdd(&ws.diag[22], (unsigned long long)S.fills);
-#endif
-    }
-    wave_sync();
-    form_batch(s_qbase, s_head, s_tail, 0, 0, s_seg, &s_nseg, &s_n);
-    wave_sync();
-    const int ns = s_nseg;
-    if (s_specblk >= 0 && s_specool > 0 && lane == 0) s_specool = (int)max(0ll, (long long)s_specool - pops);
-    wave_sync();
-    // the cascade that stopped the speculative engine is done, or its cooldown is over: hand the
-    // regime back to it (as small_loop does after serial_loop)
-    const bool specgo = s_specblk >= 0 && s_specool <= 0 && ns > 0 && lowest_bucket(s_head, s_tail, 0) >= s_specblk;
-    for (int k = lane; k < NQ; k += 64) {
-      ctl->qhead[k] = s_head[k];
-      ctl->qtail[k] = s_tail[k];
-    }
-    for (int k = lane; k < ns; k += 64) ctl->seg[k] = s_seg[k];
-    int q = 0;
-#pragma unroll
-    for (int k = 0; k < NQ / 64; ++k) q += s_tail[lane + 64 * k] - s_head[lane + 64 * k];
-    q = wave_sum(q);
-    if (lane == 0) {
-      Batch nb;
-      nb.mode = 0;
-      nb.epoch = B0.epoch + 1;
-      nb.ncommit = 0;
-      nb.nchunk = 0;
-      nb.rrun = 0;
-      nb.nseg = ns;
-      nb.n = (ns > 0) ? s_n : 0;
-      nb.L = (ns > 0) ? s_seg[0].L : -1;
-      nb.bstart = (ns > 0) ? s_seg[0].bstart : 0;
-      if (specgo) {
-        spec_begin(ctl, nb, nb.L, s_qbase[nb.L] + s_head[nb.L], s_tail[nb.L] - s_head[nb.L]);
-        if (ctl->spec.fresh || ctl->spec.tstart == 0) {  // flood start, or after a cooldown: judge anew
-          ctl->spec.fresh = 0;
-          ctl->spec.accg = 0;
-          ctl->spec.tstart = (long long)__builtin_amdgcn_s_memrealtime();
-          ctl->spec.tspec = ctl->spec.pspec = 0;
-          ctl->spec.pstart = ctl->pops + pops;
-        }
-        ctl->spec.on = 1;
-        ctl->spec.block = 0;
-      }
-      ctl->bat = nb;
-      ctl->wcap = 0;  // the next batch: a whole generation (next_wcap shrinks it again on a cut)
-      if (s_specblk >= 0) ctl->spec.cool = s_specool;
-      ctl->cut = NONE;
-      ctl->segcut = NONE;
-      ctl->minpush = NQ;
-      ctl->remaining = q;
-      ctl->batches += pops;
-      ctl->pops += pops;
-      ctl->items += pops;
-      ctl->pushes += pushes;
-      ctl->lpops += pops;
-      ctl->lpushes += pushes;
-      if (s_err) ctl->error |= s_err;
-      if (nb.n == 0 && !s_err) ctl->done = 1;
-    }
-  }
-  wave_sync();
-  if (lane == 0 && ws.hmir) {
-    const Batch nb = ctl->bat;
-    __hip_atomic_store(ws.hmir + 1, ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(ws.hmir + 2, ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(ws.hmir + 3, ctl->remaining, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(ws.hmir + 4, ctl->spec.on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(ws.hmir + 5, ctl->spec_want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(ws.hmir + 6, fast_batch(nb, ctl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(ws.hmir + 7, nb.mode == 4 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // k_serial_multi: the serial pops of MANY floods in one launch (the batch entry points' many-floods
 // mode, msg_set_batch_floods): block f = one wave = flood f, each flood in its own workspace
 // (wss[f]).  Photographs and scattered seeds put cv::watershed's exact order in its serial regime
 // -- chains of dependent pops, a lone wave's memory latency per pop -- so a
 // batch of such frames is bound by the number of floods in flight: here every flood of the call
 // (hundreds), instead of the 4-8 streams over which the full engine's floods overlap.  Each wave
-// runs k_serial's pop loop (ser_run) on its flood from wherever it stands (after phase 1, or after
-// a batch of the full engine) until its queue is empty, or until run_limit consecutive pops pushed
-// nothing below their own level (batches pay again: the host finishes that flood with the full
-// engine), then writes the queue state back and forms the next batch as k_serial does.  No wave
-// waits for another: each block only touches its own flood.
-#ifndef MSEG_MULTI_LOOP
-#define MSEG_MULTI_LOOP 1  // 1: k_scan's serial_loop per flood, 0: k_serial's ser_run (round 4 A/B)
-#endif
+// runs the small-batch loop's serial pops (serial_loop) on its flood from wherever it stands
+// (after phase 1, or after a batch of the full engine) until its queue is empty, or until
+// run_limit consecutive pops pushed nothing below their own level (batches pay again: the host
+// finishes that flood with the full engine), then writes the queue state back and forms the next
+// batch.  No wave waits for another: each block only touches its own flood.  A flood of zero
+// pixels has no workspace (ctl == nullptr: flood_begin returns before binding it) and no work.
+// (Round 4 measured a form with deferred stores and LDS rings, k_serial's: album.jpg 1362 against
+// 1176 ms for this in-loop form; it was removed in round 5.)
 __global__ __launch_bounds__(64) void k_serial_multi(const Ws* __restrict__ wss, int n, int run_limit) {
   const int f = blockIdx.x;
   if (f >= n) return;
   const Ws ws = wss[f];
   Ctl* ctl = ws.ctl;
+  if (ctl == nullptr || ws.N == 0) return;
   const int lane = lane_id();
   const Batch B0 = ctl->bat;
-  if (ctl->done || ctl->error || B0.n == 0 || (B0.mode != 0 && B0.mode != 4)) return;
-#if MSEG_MULTI_LOOP
-  // the small-batch loop's own serial pops (queue state in LDS, the bucket's next 64 slots in a
-  // register, stores straight out): the in-loop form measured faster than ser_run's deferred
-  // stores and LDS rings on photographs (album.jpg 1176 against 1362 ms, round 4)
+  if (ctl->done || ctl->error || B0.n == 0 || B0.mode != 0) return;
   __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ];
   __shared__ Seg s_seg[NQ];
   __shared__ Batch s_B;
@@ -3313,78 +2801,6 @@ __global__ __launch_bounds__(64) void k_serial_multi(const Ws* __restrict__ wss,
     if (s_err) ctl->error |= s_err;
     if (nb.n == 0 && !s_err) ctl->done = 1;
   }
-#else
-  __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ];
-  __shared__ int s_bring[NQ][SER_RING];
-  __shared__ Seg s_seg[NQ];
-  __shared__ int s_nseg, s_n;
-  __shared__ int4 s_bk[NQ];
-  __shared__ unsigned long long s_ne[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int b = 64 * k + lane;
-    const int hd = ctl->qhead[b], tl = ctl->qtail[b];
-    s_qbase[b] = ctl->qbase[b];
-    s_bk[b] = make_int4(hd, tl, s_qbase[b], tl);
-    const unsigned long long m = __ballot(tl > hd);
-    if (lane == 0) s_ne[k] = m;
-  }
-  wave_sync();
-  SerStat S;
-  int err = 0;
-#if MSEG_SER_WINDOW
-  __shared__ int s_win[2][SER_WT * SER_WT * 16];
-  ser_run_w(ws, s_bk, s_bring, s_ne, err, S, 0, 1ll << 62, run_limit, s_win[0], s_win[1]);
-#else
-  ser_run(ws, s_bk, s_bring, s_ne, err, S, 0, 1ll << 62, run_limit);
-#endif
-  wave_sync();
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int4 r = s_bk[64 * k + lane];
-    s_head[64 * k + lane] = r.x;
-    s_tail[64 * k + lane] = r.y;
-  }
-  wave_sync();
-  form_batch(s_qbase, s_head, s_tail, 0, 0, s_seg, &s_nseg, &s_n);
-  wave_sync();
-  const int ns = s_nseg;
-  for (int k = lane; k < NQ; k += 64) {
-    ctl->qhead[k] = s_head[k];
-    ctl->qtail[k] = s_tail[k];
-  }
-  for (int k = lane; k < ns; k += 64) ctl->seg[k] = s_seg[k];
-  int q = 0;
-#pragma unroll
-  for (int k = 0; k < NQ / 64; ++k) q += s_tail[lane + 64 * k] - s_head[lane + 64 * k];
-  q = wave_sum(q);
-  if (lane == 0) {
-    Batch nb;
-    nb.mode = 0;
-    nb.epoch = B0.epoch + 1;
-    nb.ncommit = 0;
-    nb.nchunk = 0;
-    nb.rrun = 0;
-    nb.nseg = ns;
-    nb.n = (ns > 0) ? s_n : 0;
-    nb.L = (ns > 0) ? s_seg[0].L : -1;
-    nb.bstart = (ns > 0) ? s_seg[0].bstart : 0;
-    ctl->bat = nb;
-    ctl->wcap = 0;
-    ctl->cut = NONE;
-    ctl->segcut = NONE;
-    ctl->minpush = NQ;
-    ctl->remaining = q;
-    ctl->batches += S.pops;
-    ctl->pops += S.pops;
-    ctl->items += S.pops;
-    ctl->pushes += S.pushes;
-    ctl->lpops += S.pops;
-    ctl->lpushes += S.pushes;
-    if (err) ctl->error |= err;
-    if (nb.n == 0 && !err) ctl->done = 1;
-  }
-#endif
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -70,22 +70,15 @@ constexpr int ERR_LEFTOVER = 8;  // a queued (or phase-1) state survived the flo
 // changes (the serial result is the unique fixed point: item i depends only on items < i).
 constexpr int SPEC_WIN = 1 << 20;   // items per generation (claim ranks have 22 bits)
 constexpr int SPEC_BS = 256;        // threads per k_spec_round block
-#ifndef MSEG_SPEC_QCAP
-#define MSEG_SPEC_QCAP 32
-#endif
-#ifndef MSEG_SPEC_RL
-#define MSEG_SPEC_RL 256
-#endif
-constexpr int SPEC_QCAP = MSEG_SPEC_QCAP;  // per-lane cascade queue in LDS ("hot": the smallest keys)
-constexpr int SPEC_RL = MSEG_SPEC_RL;      // records per execution in lane scratch, the rest in pool chunks
+constexpr int SPEC_QCAP = 32;      // per-lane cascade queue in LDS ("hot": the smallest keys)
+constexpr int SPEC_RL = 256;       // records per execution in lane scratch, the rest in pool chunks
 constexpr int SPEC_CCAP = 4096;     // "cold" cascade entries of one execution (a pool chunk): more = overflow
 constexpr int SPEC_XCH = 2048;      // records per pool chunk past the first SPEC_RL
 constexpr int SPEC_NX = 4;          // such chunks per execution: more records = overflow
 constexpr int SPEC_MAXREC = SPEC_RL + SPEC_NX * SPEC_XCH;  // longest execution a lane runs
-#ifndef MSEG_SPEC_MAXREC_SHORT
-#define MSEG_SPEC_MAXREC_SHORT 256
-#endif
-constexpr int SPEC_MAXREC_SHORT = MSEG_SPEC_MAXREC_SHORT;  // ... except the stable prefix's head
+constexpr int SPEC_MAXREC_SHORT = 256;  // pops an execution may run (more: a capacity overflow,
+                                        // serial pops) -- except the stable prefix's head and, in
+                                        // deep mode, executions from round 2 on (k_spec_round)
 constexpr int SPEC_ROUNDS_MAX = 64; // rounds per generation before the stable prefix is committed
 constexpr int SPEC_FT = 1024;       // items per k_spec_flatten tile
 constexpr int SPEC_QUIET = 4096;    // a generation this large without a cascade ends the regime
@@ -134,12 +127,11 @@ struct SpecCtl {
   unsigned long long rmax;  // diagnostics: longest wave of this round (10 ns ticks) | waits | cascades
   unsigned long long rmax2; // ... | its dealing + promotion | its post-execution work
   int ov1, ov2;             // lowest overflowing rank of the last / the one-before-last round
-  int longcap;              // executions may run SPEC_MAXREC pops (else Ws.spec_maxrec): set by a
-                            // fallback, cleared by a generation whose executions all stayed short
-  int xmax;                 // longest execution (pops) of the current generation, all rounds
   int deep;                 // 1: from round 2 on every execution may run SPEC_MAXREC pops; set
                             // by the flood's first cooldown, 2 (off for good) by a second one
   long long replays;        // executions whose cascade was replayed from the previous round
+  long long xpops;          // pops k_spec_round ran pop by pop (top pops + cascade pops of the
+                            // executions that were not replayed): its algorithmic unit
 };
 
 // desc word of a batch item: bits 0-31 the 4 edge weights, 32-35 push (or 0-neighbour) mask,
@@ -166,7 +158,7 @@ struct Batch {
   int ncommit;     // committed prefix (set by k_scan)
   int nchunk;      // chunks of the committed prefix (set by k_scan)
   int mode;        // 0 = flood batch, 1 = phase-1 pseudo-batch (items = ilist), 3 = speculative
-                   // generation, 4 = serial pops pending (k_serial)
+                   // generation
   int rrun;        // k_resolve re-runs of this batch so far (chunks given up: see k_resolve)
 };
 
@@ -218,7 +210,9 @@ struct Ctl {
   // critical paths: k_commit_fast's share is what the other paths leave (no atomics in it)
   long long spops, s0pops, spushes;  // committed by k_scan + k_scatter: all modes, flood batches only
   long long lpops, lpushes;          // popped one workgroup / one wave at a time (k_scan's loop,
-                                     // k_serial, k_serial_multi)
+                                     // k_serial_multi)
+  long long ritems;                  // items of the batches k_resolve decided (re-runs included):
+                                     // k_resolve's algorithmic unit
 };
 
 static_assert(__builtin_offsetof(Ctl, error) % 8 == 0 && __builtin_offsetof(Ctl, rgive) == __builtin_offsetof(Ctl, error) + 4,
@@ -242,7 +236,7 @@ struct Ws {
   Ctl* ctl;
   unsigned long long* diag;  // nullptr = off; else 8 counters (msg_set_diag)
   int* hmir;         // host-mapped progress mirror {iteration, done, error, remaining, spec, spec_want,
-                     // fast batch, serial pending}
+                     // fast batch}
   // speculative generations (nullptr when the engine is off): one 32-byte record per tiled
   // pixel (indexed like mk) holding both round parities' claims and labels and the final claim,
   // so that a pixel's view is one 128-B line instead of five arrays
@@ -259,7 +253,6 @@ struct Ws {
   long long snp;
   long long slogcap;
   int spec_lazy;     // 1: engine enabled, workspace not allocated yet (k_scan reports spec_want)
-  int serk;          // 1: the serial-pop regime runs in k_serial (mode 4), 0: inside k_scan
   int H, W;
   int Wt;            // tiles per tile row = ceil(W / 4)
   int marg;          // tiled entries of margin before mk / w4 (mk - marg starts the state array)
@@ -270,8 +263,6 @@ struct Ws {
   unsigned long long* sxp;   // chunk pool of a round: an execution's cold cascade queue (SPEC_CCAP
                              // keys) and its records past SPEC_RL (SPEC_XCH each), reset every round
   long long sxcap;
-  int spec_maxrec;           // pops an execution may run (more: a capacity overflow -> serial pops)
-  int spec_capmode;          // when executions may run SPEC_MAXREC pops instead (k_spec_round)
   int multi;                 // 1: a flood of a many-floods batch: k_scan stops after each commit (no
                              // small-batch loop), k_serial_multi pops it together with the others
 };

@@ -128,10 +128,6 @@ class Segmenter:
         """Two-launch iterations for large flood batches (default on); off = three launches."""
         self._check(self._L.msg_set_fast_commit(self._h, 1 if on else 0))
 
-    def set_serial_kernel(self, on=True):
-        """Serial-pop regime in k_serial, one wave (default off: the pops run inside k_scan)."""
-        self._check(self._L.msg_set_serial_kernel(self._h, 1 if on else 0))
-
     def set_speculative(self, on=True):
         """Speculative generations for the interrupt-dense regime (default on); off = serial pops."""
         self._check(self._L.msg_set_speculative(self._h, 1 if on else 0))

@@ -38,7 +38,7 @@ EXPORTS = (
     "msg_watershed", "msg_colorize", "msg_watershed_colorize", "msg_watershed_batch",
     "msg_watershed_dev", "msg_colorize_dev", "msg_watershed_colorize_dev", "msg_edge_weights_dev",
     "msg_set_profiling", "msg_get_kernel_profile", "msg_set_diag", "msg_set_speculative",
-    "msg_set_fast_commit", "msg_set_serial_kernel",
+    "msg_set_fast_commit",
     "msg_set_batch_inflight", "msg_set_batch_floods", "msg_set_resolve_grid", "msg_watershed_colorize_batch_dev",
     "msg_gray_hist_dev", "msg_nc_levels", "msg_nc_marker_lut", "msg_nc_markers_dev",
     "msg_nc_marker_stage_dev", "msg_nc_marker_stage",
@@ -66,7 +66,8 @@ class Stats(ctypes.Structure):
                 ("spec_cooldowns", ctypes.c_int64), ("spec_gen_pops", ctypes.c_int64),
                 ("spec_gen_us", ctypes.c_int64),
                 ("fast_pops", ctypes.c_int64), ("fast_pushes", ctypes.c_int64),
-                ("scatter_pops", ctypes.c_int64), ("scatter_pushes", ctypes.c_int64)]
+                ("scatter_pops", ctypes.c_int64), ("scatter_pushes", ctypes.c_int64),
+                ("resolve_items", ctypes.c_int64), ("spec_exec_pops", ctypes.c_int64)]
 
 
 class KernelProfile(ctypes.Structure):
@@ -79,7 +80,7 @@ class BrightLevel(ctypes.Structure):
     _fields_ = [("start", ctypes.c_int32), ("end", ctypes.c_int32), ("count", ctypes.c_int32)]
 
 
-NKERNELS = 25  # MSG_NKERNELS (include/msegment.h; tests/test_abi.py checks the two agree)
+NKERNELS = 24  # MSG_NKERNELS (include/msegment.h; tests/test_abi.py checks the two agree)
 
 
 def build(arch="gfx950"):
@@ -165,8 +166,6 @@ def load():
     L.msg_set_speculative.restype = i
     L.msg_set_fast_commit.argtypes = [vp, i]
     L.msg_set_fast_commit.restype = i
-    L.msg_set_serial_kernel.argtypes = [vp, i]
-    L.msg_set_serial_kernel.restype = i
     L.msg_get_kernel_profile.argtypes = [vp, ctypes.POINTER(KernelProfile), i, i]
     L.msg_get_kernel_profile.restype = i
     L.msg_set_batch_inflight.argtypes = [vp, i]

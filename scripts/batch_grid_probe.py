@@ -1,7 +1,7 @@
-"""Config 5 per GPU (8 mosaic 4096^2 frames per call) against the k_resolve grid size, the commit
-grid's share (MSEG_BATCH_COMMIT_SUBS; default: 1/k of the chip) and the number of floods in flight:
-does a smaller per-flood grid let concurrent floods share the chip?
-usage: python scripts/batch_grid_probe.py [commit_subs,...]   (0 = the default share)"""
+"""Config 5 per GPU (8 mosaic 4096^2 frames per call) against the k_resolve grid size and the number
+of floods in flight: does a smaller per-flood grid let concurrent floods share the chip?
+(Round 4 also swept the commit grid's share through an environment knob, since removed.)
+usage: python scripts/batch_grid_probe.py"""
 import os
 import sys
 import time
@@ -25,25 +25,19 @@ def main():
     labs = [torch.empty_like(m) for m in mks]
     dsts = [torch.empty((S, S, 3), dtype=torch.uint8, device=dev) for _ in frames]
     depth = max(f[2] for f in frames)
-    csubs = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0]
-    for cs in csubs:
-        if cs:
-            os.environ["MSEG_BATCH_COMMIT_SUBS"] = str(cs)
-        else:
-            os.environ.pop("MSEG_BATCH_COMMIT_SUBS", None)
-        for grid in (0, 384, 256, 128):
-            for inflight in (4, 8):
-                seg.set_resolve_grid(grid)
-                seg.set_batch_inflight(inflight)
+    for grid in (0, 384, 256, 128):
+        for inflight in (4, 8):
+            seg.set_resolve_grid(grid)
+            seg.set_batch_inflight(inflight)
+            seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(3):
                 seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                for _ in range(3):
-                    seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)
-                torch.cuda.synchronize()
-                dt = (time.perf_counter() - t0) / 3
-                print("commit subs %4s  resolve grid %4s  in flight %d: %7.0f Mpx/s"
-                      % (cs or "dflt", grid or "dflt", inflight, K * S * S / dt / 1e6), flush=True)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / 3
+            print("resolve grid %4s  in flight %d: %7.0f Mpx/s" % (grid or "dflt", inflight, K * S * S / dt / 1e6),
+                  flush=True)
 
 
 if __name__ == "__main__":
