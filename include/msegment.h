@@ -163,12 +163,21 @@ int msg_watershed_colorize(msg_ctx* ctx, const uint8_t* bgr, size_t bgr_stride,
 int msg_watershed_batch(msg_ctx* ctx, int n, const uint8_t* const* bgr, const size_t* bgr_stride,
                         int32_t* const* markers, const size_t* marker_stride, const int* rows,
                         const int* cols);
+/* The same batch with each frame's colorByIndexes (one palette for every frame, NULL = white;
+ * dst_bgr[k] rows*cols*3 bytes at dst_stride[k]): the reference's evaluation loop floods 92
+ * frames per image through PictureService.watershed (CorrelationTestService.java:84-86, 116, 128,
+ * 141 -> PictureService.java:852), which the JNI shim hands over in one call
+ * (MSegmentNative.watershedBatch). */
+int msg_watershed_colorize_batch(msg_ctx* ctx, int n, const uint8_t* const* bgr, const size_t* bgr_stride,
+                                 int32_t* const* markers, const size_t* marker_stride, const int* rows,
+                                 const int* cols, int depth, const uint8_t* palette_bgr,
+                                 uint8_t* const* dst_bgr, const size_t* dst_stride);
 
 /* Floods kept in flight by the batch entry points (1..8, default 4; 1 = back to back). */
 int msg_set_batch_inflight(msg_ctx* ctx, int k);
 
 /* Many floods per launch in the batch entry points (msg_watershed_batch,
- * msg_watershed_colorize_batch_dev), for frames whose exact flood is serial-bound -- photographs,
+ * msg_watershed_colorize_batch, msg_watershed_colorize_batch_dev), for frames whose exact flood is serial-bound -- photographs,
  * the scattered seeds of notConnectedMarkers (PictureService.java:852, called 90 times per image by
  * CorrelationTestService.java:84-86, 141): every frame of the call gets a workspace of its own
  * (~44 B/px of HBM each), and ONE kernel pops all of them, one wave per flood, so the call keeps

@@ -1399,65 +1399,111 @@ int msg_colorize(msg_ctx* c, const int32_t* labels, size_t label_stride, int row
   return MSG_OK;
 }
 
-int msg_watershed_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size_t* bgr_stride,
-                        int32_t* const* markers, const size_t* marker_stride, const int* rows,
-                        const int* cols) {
+}  // extern "C"
+
+namespace {
+
+// The host-buffer batch (msg_watershed_batch, msg_watershed_colorize_batch): labels in place, and
+// the colourised frames when dst is given.  Many-floods mode: every frame staged (image, markers,
+// colour output, each 16-B aligned), flooded together, read back; otherwise run_batch.
+int host_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size_t* bgr_stride, int32_t* const* markers,
+               const size_t* marker_stride, const int* rows, const int* cols, int depth, const uint8_t* palette,
+               uint8_t* const* dst, const size_t* dst_stride) {
   if (!c || n < 0) return MSG_EINVAL;
   if (n > 0 && (!bgr || !bgr_stride || !markers || !marker_stride || !rows || !cols))
     return fail(c, MSG_EINVAL, "null batch array");
-  if (c->many && n > 0) {
-    // every frame staged (image, then its markers 16-B aligned), flooded in place together
-    std::vector<long long> off(n + 1, 0);
-    for (int k = 0; k < n; ++k) {
-      const int rc = host_args(c, bgr[k], bgr_stride[k], markers[k], marker_stride[k], rows[k], cols[k], true);
-      if (rc) return rc;
-      const long long N = (long long)rows[k] * cols[k];
-      off[k + 1] = off[k] + ((3 * N + 15) & ~15ll) + 4 * N;
-    }
-    HIPCHK(c, hipSetDevice(c->dev));
-    if (off[n] > c->mstage_cap) {
-      dfree(c->d_mstage);
-      c->mstage_cap = 0;
-      HIPCHK(c, hipMalloc((void**)&c->d_mstage, off[n] + 16));
-      c->mstage_cap = off[n];
-    }
-    auto img_of = [&](int k) { return c->d_mstage + off[k]; };
-    auto mk_of = [&](int k) {
-      return (int32_t*)(c->d_mstage + off[k] + ((3ll * rows[k] * cols[k] + 15) & ~15ll));
-    };
-    hipStream_t st = c->own;
-    for (int k = 0; k < n; ++k) {
-      if ((long long)rows[k] * cols[k] == 0) continue;
-      HIPCHK(c, hipMemcpy2DAsync(img_of(k), (size_t)cols[k] * 3, bgr[k], bgr_stride[k], (size_t)cols[k] * 3,
-                                 rows[k], hipMemcpyHostToDevice, st));
-      HIPCHK(c, hipMemcpy2DAsync(mk_of(k), (size_t)cols[k] * 4, markers[k], marker_stride[k],
-                                 (size_t)cols[k] * 4, rows[k], hipMemcpyHostToDevice, st));
-    }
-    HIPCHK(c, hipStreamSynchronize(st));  // the floods run on the sub-contexts' streams
-    int rc = batch_many(c, n, 0, nullptr,
-                        [&](int k, const uint8_t*& img, const int32_t*& mk, int& H, int& W, int32_t*& lab, uint8_t*& dst) {
-                          img = img_of(k);
-                          mk = mk_of(k);
-                          H = rows[k];
-                          W = cols[k];
-                          lab = mk_of(k);
-                          dst = nullptr;
-                        });
+  if (n > 0 && dst && !dst_stride) return fail(c, MSG_EINVAL, "null batch array");
+  if (dst && depth < 0) return fail(c, MSG_EINVAL, "negative depth");
+  for (int k = 0; k < n; ++k) {
+    const int rc = host_args(c, bgr[k], bgr_stride[k], markers[k], marker_stride[k], rows[k], cols[k], true);
     if (rc) return rc;
-    for (int k = 0; k < n; ++k) {
-      if ((long long)rows[k] * cols[k] == 0) continue;
-      HIPCHK(c, hipMemcpy2DAsync(markers[k], marker_stride[k], mk_of(k), (size_t)cols[k] * 4, (size_t)cols[k] * 4,
-                                 rows[k], hipMemcpyDeviceToHost, st));
-    }
-    HIPCHK(c, hipStreamSynchronize(st));
-    for (int k = 0; k < n; ++k)
-      for (int j = 0; j < cols[k] && rows[k] > 0; ++j)
-        if (markers[k][j] != WSHED) return fail(c, MSG_ESTATE, "label read-back of frame %d failed the frame-border check", k);
-    return MSG_OK;
+    if (dst && (long long)rows[k] * cols[k] > 0 && (!dst[k] || dst_stride[k] < (size_t)cols[k] * 3))
+      return fail(c, MSG_EINVAL, "dst of frame %d: null or stride too small", k);
   }
-  return run_batch(c, n, [&](int k, msg_ctx* x) {
-    return msg_watershed(x, bgr[k], bgr_stride[k], markers[k], marker_stride[k], rows[k], cols[k]);
-  });
+  if (!(c->many && n > 0))
+    return run_batch(c, n, [&](int k, msg_ctx* x) {
+      return dst ? msg_watershed_colorize(x, bgr[k], bgr_stride[k], markers[k], marker_stride[k], rows[k], cols[k],
+                                          depth, palette, dst[k], dst_stride[k], nullptr, 0)
+                 : msg_watershed(x, bgr[k], bgr_stride[k], markers[k], marker_stride[k], rows[k], cols[k]);
+    });
+  // every frame staged (image, then its markers, then its colour output, each 16-B aligned),
+  // flooded in place together
+  auto al = [](long long b) { return (b + 15) & ~15ll; };
+  std::vector<long long> off(n + 1, 0);
+  for (int k = 0; k < n; ++k) {
+    const long long N = (long long)rows[k] * cols[k];
+    off[k + 1] = off[k] + al(3 * N) + al(4 * N) + (dst ? al(3 * N) : 0);
+  }
+  HIPCHK(c, hipSetDevice(c->dev));
+  if (off[n] > c->mstage_cap) {
+    dfree(c->d_mstage);
+    c->mstage_cap = 0;
+    HIPCHK(c, hipMalloc((void**)&c->d_mstage, off[n] + 16));
+    c->mstage_cap = off[n];
+  }
+  auto img_of = [&](int k) { return c->d_mstage + off[k]; };
+  auto mk_of = [&](int k) { return (int32_t*)(c->d_mstage + off[k] + al(3ll * rows[k] * cols[k])); };
+  auto dst_of = [&](int k) {
+    const long long N = (long long)rows[k] * cols[k];
+    return c->d_mstage + off[k] + al(3 * N) + al(4 * N);
+  };
+  hipStream_t st = c->own;
+  const uint8_t* dp = nullptr;
+  if (dst && palette && depth > 0) {
+    const int rc = upload_palette(c, palette, depth, st);
+    if (rc) return rc;
+    dp = c->d_pal;
+  }
+  for (int k = 0; k < n; ++k) {
+    if ((long long)rows[k] * cols[k] == 0) continue;
+    HIPCHK(c, hipMemcpy2DAsync(img_of(k), (size_t)cols[k] * 3, bgr[k], bgr_stride[k], (size_t)cols[k] * 3,
+                               rows[k], hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpy2DAsync(mk_of(k), (size_t)cols[k] * 4, markers[k], marker_stride[k],
+                               (size_t)cols[k] * 4, rows[k], hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(c, hipStreamSynchronize(st));  // the floods run on the sub-contexts' streams
+  int rc = batch_many(c, n, depth, dp,
+                      [&](int k, const uint8_t*& img, const int32_t*& mk, int& H, int& W, int32_t*& lab, uint8_t*& d) {
+                        img = img_of(k);
+                        mk = mk_of(k);
+                        H = rows[k];
+                        W = cols[k];
+                        lab = mk_of(k);
+                        d = dst ? dst_of(k) : nullptr;
+                      });
+  if (rc) return rc;
+  for (int k = 0; k < n; ++k) {
+    if ((long long)rows[k] * cols[k] == 0) continue;
+    HIPCHK(c, hipMemcpy2DAsync(markers[k], marker_stride[k], mk_of(k), (size_t)cols[k] * 4, (size_t)cols[k] * 4,
+                               rows[k], hipMemcpyDeviceToHost, st));
+    if (dst)
+      HIPCHK(c, hipMemcpy2DAsync(dst[k], dst_stride[k], dst_of(k), (size_t)cols[k] * 3, (size_t)cols[k] * 3,
+                                 rows[k], hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(c, hipStreamSynchronize(st));
+  for (int k = 0; k < n; ++k)
+    for (int j = 0; j < cols[k] && rows[k] > 0; ++j)
+      if (markers[k][j] != WSHED) return fail(c, MSG_ESTATE, "label read-back of frame %d failed the frame-border check", k);
+  return MSG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int msg_watershed_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size_t* bgr_stride,
+                        int32_t* const* markers, const size_t* marker_stride, const int* rows,
+                        const int* cols) {
+  return host_batch(c, n, bgr, bgr_stride, markers, marker_stride, rows, cols, 0, nullptr, nullptr, nullptr);
+}
+
+int msg_watershed_colorize_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size_t* bgr_stride,
+                                 int32_t* const* markers, const size_t* marker_stride, const int* rows,
+                                 const int* cols, int depth, const uint8_t* palette_bgr, uint8_t* const* dst_bgr,
+                                 const size_t* dst_stride) {
+  if (c && n > 0 && !dst_bgr) return fail(c, MSG_EINVAL, "null batch array");
+  return host_batch(c, n, bgr, bgr_stride, markers, marker_stride, rows, cols, depth, palette_bgr,
+                    n > 0 ? dst_bgr : nullptr, dst_stride);
 }
 
 int msg_set_resolve_grid(msg_ctx* c, int blocks) {

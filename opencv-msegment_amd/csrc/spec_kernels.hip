@@ -71,6 +71,15 @@ __device__ __forceinline__ void st_ag32(int* p, int v) {
 __device__ __forceinline__ void claim_max(unsigned long long* p, unsigned long long k) {
   __hip_atomic_fetch_max(p, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Wait for every vector memory operation of the wave (s_waitcnt vmcnt(0); expcnt and lgkmcnt left
+// alone).  A pop's loads are waited for explicitly BEFORE the previous pop's claims, label and
+// record are issued: the counter retires in issue order, and with those writes issued after the
+// loads in branches some lanes (or the whole wave) skip, the compiler's own wait at the first use
+// of a loaded value is vmcnt(0) behind the writes too -- their acknowledgements (atomics at the L2
+// or beyond) then sat on every pop's critical path.  Issued after the wait, the writes complete
+// while the pop is decided and the next pop's loads are in flight.
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 __device__ __forceinline__ unsigned long long fin_word(unsigned G, unsigned popped, int lab) {
   return ((unsigned long long)G << 33) | ((unsigned long long)popped << 32) | (uint32_t)lab;
 }
@@ -238,6 +247,333 @@ __device__ void spec_finalize(Ctl* ctl, int P, int n, unsigned T, unsigned G, un
     ctl->sxtop.v = 0;  // every execution of this round has copied its records to the log
   }
   s.ticket = 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wave-cooperative cascades (round 5).  A round lasts as long as its longest execution, and that
+// execution is usually one lane's long cascade running alone in its wave after the other 63
+// lanes' executions ended: round 4 measured ~7000 wave cycles per lone-lane cascade pop (a serial
+// scan of the lane's 32 hot keys, four neighbour records decided one after another, the claims and
+// the record written by one lane), against one dependent memory round trip that a pop needs.
+// When a single lane of the wave is left with a cascade, the whole wave takes its execution over
+// and finishes it with the SAME pop sequence -- the cascade's serial order (lowest level first,
+// FIFO within a level) is a property of the keys, not of who pops them:
+//   * queue: the wave's 64 LDS columns (the per-lane queues of the finished lanes, 2048 slots)
+//     hold the hot entries {ord = level << 16 | push sequence, pixel}, any lane's column, each
+//     lane tracking its column's smallest ord; the next pop is a DPP wave minimum over those, and
+//     the popped column's new minimum is found by the wave in parallel while the pop's loads are
+//     in flight.  Cold keys stay in the execution's pool chunk (every cold key larger than every
+//     hot one, as in the per-lane queue); an empty hot set takes every cold key up to the largest
+//     level that fits back in one parallel pass (level histogram in LDS, then a scatter);
+//   * a pop: lanes 0-3 load and decide one neighbour each (the same spec_decide, patched with the
+//     previous pop's writes, which are issued after these loads exactly as in the per-lane loop),
+//     the fold and the pushes are uniform, and the claims, label and record go out as one masked
+//     instruction each;
+//   * capacities: 2048 hot entries (more: a capacity overflow, as a lane's 32 + 4096), the cold
+//     chunk and the record chunks exactly as in the per-lane loop, and the same length caps.
+// The execution's results (records, signature, overflow flags, record chunks) land where the
+// per-lane loop leaves them, so the rest of the round does not know which form ran it.
+constexpr int COOP_HOT = SPEC_QCAP * 64;  // hot slots of a cooperating wave (its LDS columns)
+constexpr int COOP_MAXORD = 0x7fffffff;
+static_assert(4 * SPEC_MAXREC < (1 << 16), "an execution's push sequence fits the 16 bits of a coop ord");
+
+struct CoopSt {
+  int y;                      // the pop selected next (already out of the queue)
+  int py, plab;               // the previous pop: pixel, label, pushes (for the patch) ...
+  unsigned ppm;
+  int pz0, pz1, pz2, pz3;
+  unsigned long long prec;    // ... its record, and whether its writes are still to be issued
+  bool pwrite;
+  int nrec;
+  unsigned long long sig;
+  unsigned qseq;
+  int nq;                     // hot keys in the owner's LDS column (per-lane format), at entry
+  int nc, cb;                 // cold keys in the pool chunk cb (-1 none yet, -2 pool full)
+  unsigned cmin;
+  int xb0, xb1, xb2, xb3;     // record chunks past SPEC_RL
+  bool ovf, cap;
+};
+
+// lq: the block's per-lane queues ([entry][thread]); wb: the wave's first thread; w: the owner lane.
+__device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsigned long long* lq, int wb,
+                                                    int w, int j, int L, bool longok, unsigned long long* tmp,
+                                                    CoopSt& S) {
+  Ctl* const ctl = ws.ctl;
+  const int lane = lane_id();
+  const int Wt = ws.Wt, marg = ws.marg;
+  const unsigned T = V.T;
+  const int par = V.par;
+  SpecPx* const spx = const_cast<SpecPx*>(V.spx);
+  unsigned long long* const col = lq + wb + lane;  // this lane's column: entry e at col[e * SPEC_BS]
+  auto pool_get = [&](int sz) -> int {             // lane 0 asks, the wave gets the answer
+    int b = -1;
+    if (lane == 0 && ld_ag32(&ctl->sxtop.v) < ws.sxcap) {
+      b = atomicAdd(&ctl->sxtop.v, sz);
+      if (b < 0 || (long long)b + sz > ws.sxcap) b = -1;
+    }
+    return __builtin_amdgcn_readlane(b, 0);
+  };
+  // ---- entry: the owner's hot keys become coop entries, one per lane (lane e takes row e) ----
+  int cnt = 0, m1 = COOP_MAXORD, m1row = 0, m1pix = 0;
+  {
+    const unsigned long long k = (lane < S.nq) ? lq[(size_t)lane * SPEC_BS + wb + w] : 0ull;
+    if (lane < S.nq) {
+      const int ord = (int)(((k >> 52) << 16) | ((k >> 28) & 0xffffu));
+      m1pix = (int)(k & 0x0fffffffu);
+      col[0] = ((unsigned long long)(unsigned)ord << 32) | (unsigned)m1pix;
+      cnt = 1;
+      m1 = ord;
+    }
+  }
+  int H = S.nq, rr = S.nq & 63;
+  int fix = -1;  // a column whose minimum was popped: refilled hole + new minimum still to be found
+  auto rec_at = [&](int k) { return spec_rec_at(tmp, ws.sxp, k, S.xb0, S.xb1, S.xb2, S.xb3); };
+  auto cold_add = [&](unsigned t, int pix, unsigned seq) {
+    if (S.cb == -2 || S.nc >= SPEC_CCAP) {
+      S.ovf = S.cap = true;
+      return;
+    }
+    if (S.cb < 0 && (S.cb = pool_get(SPEC_CCAP)) < 0) {
+      S.cb = -2;
+      S.ovf = S.cap = true;
+      return;
+    }
+    if (lane == 0)
+      ws.sxp[(size_t)S.cb + S.nc] =
+          ((unsigned long long)t << 52) | ((unsigned long long)(seq & 0xffffffu) << 28) | (unsigned)pix;
+    ++S.nc;
+    S.cmin = min(S.cmin, t);
+  };
+  auto qpush = [&](unsigned t, int pix) {
+    const unsigned seq = S.qseq++;
+    if (S.nc > 0 && t >= S.cmin) {  // above the smallest cold key: cold too
+      cold_add(t, pix, seq);
+      return;
+    }
+    if (H >= COOP_HOT) {
+      S.ovf = S.cap = true;
+      return;
+    }
+    // the next column with room, round robin from rr
+    const unsigned long long room = __ballot(cnt < SPEC_QCAP);
+    const unsigned long long hi = room & (~0ull << rr);
+    const int tl = hi ? __builtin_ctzll(hi) : __builtin_ctzll(room);
+    const int ord = (int)((t << 16) | (seq & 0xffffu));
+    if (lane == tl) {
+      col[(size_t)cnt * SPEC_BS] = ((unsigned long long)(unsigned)ord << 32) | (unsigned)pix;
+      if (ord < m1) {
+        m1 = ord;
+        m1row = cnt;
+        m1pix = pix;
+      }
+      ++cnt;
+    }
+    ++H;
+    rr = (tl + 1) & 63;
+  };
+  // hot empty, cold not: every cold key up to the largest level whose count still fits the hot
+  // slots moves hot (the rest stay cold: all larger than every hot key)
+  auto refill = [&]() {
+    unsigned* const hb = reinterpret_cast<unsigned*>(lq);  // 256 level bins in rows 0-1 of the columns
+    auto bin = [&](int b) -> unsigned* { return hb + ((size_t)(b >> 7) * SPEC_BS + wb) * 2 + (b & 127); };
+#pragma unroll
+    for (int k = 0; k < 4; ++k) *bin(4 * lane + k) = 0u;
+    const size_t cb = (size_t)S.cb;
+    for (int b0 = 0; b0 < S.nc; b0 += 64) {
+      if (b0 + lane < S.nc) atomicAdd(bin((int)(ws.sxp[cb + b0 + lane] >> 52)), 1u);
+    }
+    int h[4], s4 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      h[k] = (int)*bin(4 * lane + k);
+      s4 += h[k];
+    }
+    int c = wave_scan_add(s4) - s4;  // keys below level 4 * lane
+    int best = -1, movc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c += h[k];
+      if (c <= COOP_HOT) {
+        best = 4 * lane + k;
+        movc = c;
+      }
+    }
+    const int vstar = -wave_min(-best);  // the largest level whose cumulative count fits
+    const unsigned long long bw = __ballot(best == vstar);
+    const int M = __builtin_amdgcn_readlane(movc, __builtin_ctzll(bw));
+    if (vstar < (int)S.cmin || M == 0) {  // the lowest cold level alone is larger than the hot slots
+      S.ovf = S.cap = true;
+      return;
+    }
+    int moved = 0, kept = 0;
+    unsigned ncmin = 256;
+    for (int b0 = 0; b0 < S.nc; b0 += 64) {
+      const bool valid = b0 + lane < S.nc;
+      const unsigned long long k = valid ? ws.sxp[cb + b0 + lane] : 0ull;
+      const unsigned lv = (unsigned)(k >> 52);
+      const bool mv = valid && (int)lv <= vstar, kp = valid && !mv;
+      const unsigned long long bm = __ballot(mv), bk = __ballot(kp);
+      if (mv) {
+        const int pos = moved + lanes_below(bm);
+        const int ord = (int)((lv << 16) | ((k >> 28) & 0xffffu));
+        lq[(size_t)(pos >> 6) * SPEC_BS + wb + (pos & 63)] =
+            ((unsigned long long)(unsigned)ord << 32) | (unsigned)(k & 0x0fffffffu);
+      }
+      if (kp) {
+        ws.sxp[cb + kept + lanes_below(bk)] = k;
+        ncmin = min(ncmin, lv);
+      }
+      moved += __popcll(bm);
+      kept += __popcll(bk);
+    }
+    S.nc = kept;
+    S.cmin = (unsigned)wave_min((int)ncmin);
+    H = moved;
+    cnt = (moved >> 6) + (lane < (moved & 63) ? 1 : 0);
+    rr = moved & 63;
+    m1 = COOP_MAXORD;
+    for (int e = 0; e < cnt; ++e) {
+      const unsigned long long x = col[(size_t)e * SPEC_BS];
+      if ((int)(x >> 32) < m1) {
+        m1 = (int)(x >> 32);
+        m1row = e;
+        m1pix = (int)(unsigned)x;
+      }
+    }
+  };
+  int y = S.y;
+#ifdef MSEG_SPEC_PROF
+  const long long c_t0 = (long long)__builtin_amdgcn_s_memtime();
+  const int c_n0 = S.nrec;
+#endif
+  for (;;) {
+    // ---- the length caps and the record chunk of pop nrec, as at the per-lane loop's head ----
+    if (S.nrec >= (longok ? SPEC_MAXREC : SPEC_MAXREC_SHORT)) {
+      S.ovf = S.cap = true;
+      break;
+    }
+    if (S.nrec >= SPEC_RL && (S.nrec - SPEC_RL) % SPEC_XCH == 0) {
+      const int c = (S.nrec - SPEC_RL) / SPEC_XCH;
+      const int b = c < SPEC_NX ? pool_get(SPEC_XCH) : -1;
+      if (b < 0) {
+        S.ovf = S.cap = true;
+        break;
+      }
+      if (c == 0) S.xb0 = b;
+      else if (c == 1) S.xb1 = b;
+      else if (c == 2) S.xb2 = b;
+      else S.xb3 = b;
+    }
+    // ---- the pop of y: its loads (lanes 0-3 one neighbour each), then the previous pop's writes ----
+    const int yb = y + marg;
+    const int nbd = nbi(yb, lane & 3, Wt) - marg;
+    SpecRec r;
+    unsigned wyl = 0;
+    if (lane < 4) {
+      wyl = (unsigned)ws.w4[y];
+      r = spec_load(ws, V, nbd);
+    }
+    if (fix >= 0) {  // the column the last select popped from: fill its hole, find its new minimum
+      if (lane == fix) {
+        --cnt;
+        if (m1row != cnt) col[(size_t)m1row * SPEC_BS] = col[(size_t)cnt * SPEC_BS];
+      }
+      const int co = __builtin_amdgcn_readlane(cnt, fix);
+      const unsigned long long x = (lane < co) ? lq[(size_t)lane * SPEC_BS + wb + fix] : 0ull;
+      const int ord = (lane < co) ? (int)(x >> 32) : COOP_MAXORD;
+      const int mo = wave_min(ord);
+      const unsigned long long bo = __ballot(lane < co && ord == mo);
+      const int row = bo ? __builtin_ctzll(bo) : 0;
+      const int pixo = __builtin_amdgcn_readlane((int)(unsigned)x, row);
+      if (lane == fix) {
+        m1 = co > 0 ? mo : COOP_MAXORD;
+        m1row = row;
+        m1pix = pixo;
+      }
+      fix = -1;
+    }
+    vm_drain();
+    if (S.pwrite) {  // claims of the previous pop, its label and its record: one instruction each
+      const int d = lane - 2;
+      const int zl = d == 0 ? S.pz0 : d == 1 ? S.pz1 : d == 2 ? S.pz2 : S.pz3;
+      if (lane == 0) claim_max(&spx[S.py].cl[par], spec_claim(T, j, 1u));
+      else if (d >= 0 && d < 4 && ((S.ppm >> d) & 1u)) claim_max(&spx[zl].cl[par], spec_claim(T, j, 0u));
+      if (lane == 1) st_ag32(&spx[S.py].lab[par], S.plab);
+      if (lane == 6) *rec_at(S.nrec - 1) = S.prec;
+      S.pwrite = false;
+    }
+    // ---- decide: lanes 0-3, patched with the previous pop's writes (issued after these loads) ----
+    int v = 0;
+    if (lane < 4) {
+      v = spec_decide(V, r, j, true);
+      if (nbd == S.py) v = S.plab;
+      if (((S.ppm & 1u) && nbd == S.pz0) || ((S.ppm & 2u) && nbd == S.pz1) || ((S.ppm & 4u) && nbd == S.pz2) ||
+          ((S.ppm & 8u) && nbd == S.pz3))
+        v = INQ;
+    }
+    const unsigned wy = (unsigned)__builtin_amdgcn_readfirstlane((int)wyl);
+    int vd[4], nb[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      vd[d] = __builtin_amdgcn_readlane(v, d);
+      nb[d] = __builtin_amdgcn_readlane(nbd, d);
+    }
+    int lab = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      if (vd[d] > 0) lab = fold_lab(lab, vd[d]);
+    if (lab == 0) {  // own writes hidden by a conflicting lower rank: unstable
+      S.ovf = true;
+      lab = WSHED;
+    }
+    unsigned dmy = 0, pmy = 0;
+    if (lab != WSHED) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        if (vd[d] != 0) continue;
+        pmy |= 1u << d;
+        const unsigned t = (wy >> (8 * d)) & 255u;
+        if ((int)t < L) qpush(t, nb[d]);
+        else dmy |= 1u << d;
+      }
+    }
+    S.prec = srec_pack(y, lab, dmy);
+    S.sig = smix(S.sig, S.prec);
+    S.py = y;
+    S.plab = lab;
+    S.ppm = pmy;
+    S.pz0 = nb[0];
+    S.pz1 = nb[1];
+    S.pz2 = nb[2];
+    S.pz3 = nb[3];
+    S.pwrite = true;
+    ++S.nrec;
+    if (S.ovf || H + S.nc == 0) break;
+    // ---- select: the smallest ord of all columns ----
+    if (H == 0) {
+      refill();
+      if (S.ovf) break;
+    }
+    const int m = wave_min(m1);
+    fix = __builtin_ctzll(__ballot(m1 == m));
+    y = __builtin_amdgcn_readlane(m1pix, fix);
+    --H;
+  }
+  if (S.pwrite) {  // the last pop's writes
+    const int d = lane - 2;
+    const int zl = d == 0 ? S.pz0 : d == 1 ? S.pz1 : d == 2 ? S.pz2 : S.pz3;
+    if (lane == 0) claim_max(&spx[S.py].cl[par], spec_claim(T, j, 1u));
+    else if (d >= 0 && d < 4 && ((S.ppm >> d) & 1u)) claim_max(&spx[zl].cl[par], spec_claim(T, j, 0u));
+    if (lane == 1) st_ag32(&spx[S.py].lab[par], S.plab);
+    if (lane == 6) *rec_at(S.nrec - 1) = S.prec;
+    S.pwrite = false;
+  }
+#ifdef MSEG_SPEC_PROF
+  if (ws.diag && lane == 0) {  // bank 2: cooperative pops, their cycles
+    atomicAdd(&ws.diag[21], (unsigned long long)(S.nrec - c_n0));
+    atomicAdd(&ws.diag[22], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - c_t0));
+  }
+#endif
 }
 
 // One round.  Waves take 64 consecutive ranks at a time from [Pold, n) in dispatch order:
@@ -452,13 +788,13 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
     int rbase = -1;  // >= 0: the cascade was replayed from the previous round's log records here
     int xb0 = -1, xb1 = -1, xb2 = -1, xb3 = -1;  // record chunks past SPEC_RL (SPEC_NX = 4)
 #define rec_at(k) spec_rec_at(tmp, ws.sxp, (k), xb0, xb1, xb2, xb3)
-    if (ex) {
+    {
       // ---- the top pop, then the cascade (levels < L, lowest first, FIFO) ----
       // Every pop's writes (claims, label, record) are issued AFTER the loads of the next pop's
-      // neighbours: the wave's memory counter retires in issue order, so a load issued behind
-      // stores waits for their acknowledgements too.  The next pop therefore sees its
-      // predecessor's writes through a patch (that pop's pixel and pushes) instead of memory;
-      // everything older was issued before its loads.
+      // neighbours have completed (vm_drain): the wave's memory counter retires in issue order, so
+      // a load issued behind stores waits for their acknowledgements too.  The next pop therefore
+      // sees its predecessor's writes through a patch (that pop's pixel and pushes) instead of
+      // memory; everything older was issued before its loads.
       // The lane's cascade queue: keys {level, push sequence, pixel} (the serial order of a
       // cascade is the key order: lowest level first, FIFO within a level).  The SPEC_QCAP
       // smallest live keys are "hot" in LDS; the rest are "cold" in a chunk of the round's pool,
@@ -584,7 +920,7 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
         nc = w;
       };
       unsigned dm = 0, ppm = 0;  // deferred pushes; the pending pop's pushes (all levels)
-      if (mylab != WSHED) {
+      if (ex && mylab != WSHED) {
   #pragma unroll
         for (int d = 0; d < 4; ++d) {
           if (!((pm >> d) & 1u)) continue;
@@ -595,10 +931,12 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
         }
       }
       unsigned long long rec = srec_pack(p, mylab, dm);
-      sig = smix(0x6a09e667f3bcc908ull, rec);
-      nrec = 1;
+      if (ex) {
+        sig = smix(0x6a09e667f3bcc908ull, rec);
+        nrec = 1;
+      }
       // the pending pop: its writes are not issued yet
-      int py = p, plab = mylab;
+      int py = ex ? p : -1, plab = mylab;
       int pz[4] = {nbp[0], nbp[1], nbp[2], nbp[3]};
       auto issue_writes = [&](int k) {  // pop k of this execution: pixel py, label plab, pushes ppm
         claim_max(&spx[py].cl[par], spec_claim(T, j, 1u));
@@ -608,7 +946,7 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
           if ((ppm >> d) & 1u) claim_max(&spx[pz[d]].cl[par], spec_claim(T, j, 0u));
         *rec_at(k) = rec;
       };
-      if (nq > 0 && !ovf && !gchg && j < ovlim) {
+      if (ex && nq > 0 && !ovf && !gchg && j < ovlim) {
         const int4 pr = ws.srec[(size_t)ppar * SPEC_WIN + j];
         if (pr.z == (int)(T - 1u) && pr.y > 1 && ws.slog[pr.x] == rec &&
             spec_replay_clean(ws, pr.x, pr.y, ppar, T, nbp)) {
@@ -668,31 +1006,36 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
         r2 = spec_load(ws, V, nby[2]);
         r3 = spec_load(ws, V, nby[3]);
       };
-      bool more = nq + nc > 0 && !ovf;
+      bool more = ex && nq + nc > 0 && !ovf;
       if (more) {
         y = select();
         issue_loads();
       }
-      if (py >= 0) issue_writes(0);
-      while (more) {
-        // the execution length cap (see lcap above)
-        const bool longok = j == P || (lcap && T > G);
+      vm_drain();
+      if (ex && py >= 0) issue_writes(0);
+      // the execution length cap (see lcap above)
+      const bool longok = j == P || (lcap && T > G);
+      for (;;) {
+       if (more) {
+        bool go = true;
         if (nrec >= (longok ? SPEC_MAXREC : SPEC_MAXREC_SHORT)) {  // a long cascade: cheaper as serial pops
           ovf = cap = true;
-          break;
-        }
-        if (nrec >= SPEC_RL && (nrec - SPEC_RL) % SPEC_XCH == 0) {  // the next record starts a chunk
+          go = false;
+        } else if (nrec >= SPEC_RL && (nrec - SPEC_RL) % SPEC_XCH == 0) {  // the next record starts a chunk
           const int c = (nrec - SPEC_RL) / SPEC_XCH;
           const int b = c < SPEC_NX ? pool_get(SPEC_XCH) : -1;
           if (b < 0) {
             ovf = cap = true;
-            break;
+            go = false;
           }
           if (c == 0) xb0 = b;
           else if (c == 1) xb1 = b;
           else if (c == 2) xb2 = b;
           else xb3 = b;
         }
+        if (!go) more = false;
+       }
+       if (more) {
 #ifdef MSEG_SPEC_PROF
         const long long q1 = (long long)__builtin_amdgcn_s_memtime();
         pf_n += 1;
@@ -749,6 +1092,7 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
           y = select();
           issue_loads();
         }
+        vm_drain();
 #ifdef MSEG_SPEC_PROF
         const long long q4 = (long long)__builtin_amdgcn_s_memtime();
         pf_sel += q4 - q3;
@@ -757,8 +1101,56 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
 #ifdef MSEG_SPEC_PROF
         pf_write += (long long)__builtin_amdgcn_s_memtime() - q4 + (q3 - q2);
 #endif
+       }
+        // one lane left with a cascade: the wave takes it over (spec_coop) and finishes it
+        const unsigned long long bal = __ballot(more);
+        if (bal == 0) break;
+        if (__popcll(bal) == 1) {
+          const int w = __builtin_ctzll(bal);
+          CoopSt S;
+          S.y = __builtin_amdgcn_readlane(y, w);
+          S.py = __builtin_amdgcn_readlane(py, w);
+          S.plab = __builtin_amdgcn_readlane(plab, w);
+          S.ppm = (unsigned)__builtin_amdgcn_readlane((int)ppm, w);
+          S.pz0 = __builtin_amdgcn_readlane(pz[0], w);
+          S.pz1 = __builtin_amdgcn_readlane(pz[1], w);
+          S.pz2 = __builtin_amdgcn_readlane(pz[2], w);
+          S.pz3 = __builtin_amdgcn_readlane(pz[3], w);
+          S.prec = 0;
+          S.pwrite = false;  // the per-lane loop issued them
+          S.nrec = __builtin_amdgcn_readlane(nrec, w);
+          S.sig = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(sig >> 32), w) << 32) |
+                  (unsigned)__builtin_amdgcn_readlane((int)(unsigned)sig, w);
+          S.qseq = (unsigned)__builtin_amdgcn_readlane((int)qseq, w);
+          S.nq = __builtin_amdgcn_readlane(nq, w);
+          S.nc = __builtin_amdgcn_readlane(nc, w);
+          S.cb = __builtin_amdgcn_readlane(cb, w);
+          S.cmin = (unsigned)__builtin_amdgcn_readlane((int)cmin, w);
+          S.xb0 = __builtin_amdgcn_readlane(xb0, w);
+          S.xb1 = __builtin_amdgcn_readlane(xb1, w);
+          S.xb2 = __builtin_amdgcn_readlane(xb2, w);
+          S.xb3 = __builtin_amdgcn_readlane(xb3, w);
+          S.ovf = S.cap = false;
+          const int jw = __builtin_amdgcn_readlane(j, w);
+          const int wb = tid & ~63;
+          spec_coop(ws, V, lq, wb, w, jw, L, jw == P || (lcap && T > G),
+                    ws.stmp + (size_t)(blockIdx.x * SPEC_BS + wb + w) * SPEC_RL, S);
+          if (lane == w) {
+            nrec = S.nrec;
+            sig = S.sig;
+            ovf = S.ovf;
+            cap = S.cap;
+            xb0 = S.xb0;
+            xb1 = S.xb1;
+            xb2 = S.xb2;
+            xb3 = S.xb3;
+            nq = nc = 0;
+            more = false;
+          }
+          break;
+        }
       }
-    }  // ex
+    }  // the execution
     if (dg) {
       tw += tkb - tka;
       tc += (long long)__builtin_amdgcn_s_memrealtime() - tkb;

@@ -87,6 +87,81 @@ JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNativ
   return MSG_OK;
 }
 
+// msg_set_batch_floods (msegment.h): 0 = the full engine per flood, 1 / 2 = many floods per launch.
+JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_setBatchFloods(JNIEnv*, jclass,
+                                                                                                jlong ctx, jint mode) {
+  msg_ctx* c = reinterpret_cast<msg_ctx*>(ctx);
+  return c ? msg_set_batch_floods(c, mode) : MSG_EINVAL;
+}
+
+// PictureService.watershed over a batch of frames in one call (the reference's evaluation loop:
+// CorrelationTestService.java:84-86, 116, 128, 141 -> PictureService.java:852, 92 floods per
+// image): bgrs[k] (byte[]), markers[k] (int[], rewritten in place), dsts[k] (byte[]) of
+// rows[k] x cols[k]; one palette (or null = white) and depth for every frame.
+JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_watershedColorizeBatch(
+    JNIEnv* env, jclass, jlong ctx, jobjectArray bgrs, jobjectArray markers, jintArray rows, jintArray cols,
+    jint depth, jbyteArray palette, jobjectArray dsts) {
+  msg_ctx* c = reinterpret_cast<msg_ctx*>(ctx);
+  if (!c || !bgrs || !markers || !rows || !cols || !dsts || depth < 0) return MSG_EINVAL;
+  const jsize n = env->GetArrayLength(bgrs);
+  if (env->GetArrayLength(markers) != n || env->GetArrayLength(dsts) != n || env->GetArrayLength(rows) < n ||
+      env->GetArrayLength(cols) < n || (palette && env->GetArrayLength(palette) < 3ll * depth))
+    return MSG_EINVAL;
+  std::vector<jint> R, C;
+  if (!alloc(R, n) || !alloc(C, n)) return MSG_ENOMEM;
+  env->GetIntArrayRegion(rows, 0, n, R.data());
+  env->GetIntArrayRegion(cols, 0, n, C.data());
+  if (env->ExceptionCheck()) return MSG_EINVAL;
+  std::vector<std::vector<jbyte>> b(n), d(n);
+  std::vector<std::vector<jint>> m(n);
+  std::vector<jbyte> p;
+  if (palette && (!alloc(p, 3ll * depth))) return MSG_ENOMEM;
+  if (palette) env->GetByteArrayRegion(palette, 0, 3 * depth, p.data());
+  for (jsize k = 0; k < n; ++k) {
+    jbyteArray bk = static_cast<jbyteArray>(env->GetObjectArrayElement(bgrs, k));
+    jintArray mk = static_cast<jintArray>(env->GetObjectArrayElement(markers, k));
+    jbyteArray dk = static_cast<jbyteArray>(env->GetObjectArrayElement(dsts, k));
+    const bool ok = fits(env, bk, R[k], C[k], 3) && fits(env, mk, R[k], C[k], 1) && fits(env, dk, R[k], C[k], 3);
+    const long long nk = ok ? (long long)R[k] * C[k] : 0;
+    const bool mem = ok && alloc(b[k], 3 * nk) && alloc(m[k], nk) && alloc(d[k], 3 * nk);
+    if (mem) {
+      env->GetByteArrayRegion(bk, 0, (jsize)(3 * nk), b[k].data());
+      env->GetIntArrayRegion(mk, 0, (jsize)nk, m[k].data());
+    }
+    if (bk) env->DeleteLocalRef(bk);
+    if (mk) env->DeleteLocalRef(mk);
+    if (dk) env->DeleteLocalRef(dk);
+    if (!ok) return MSG_EINVAL;
+    if (!mem) return MSG_ENOMEM;
+  }
+  if (env->ExceptionCheck()) return MSG_EINVAL;
+  std::vector<const uint8_t*> bp(n);
+  std::vector<int32_t*> mp(n);
+  std::vector<uint8_t*> dp(n);
+  std::vector<size_t> bs(n), ms(n), ds(n);
+  for (jsize k = 0; k < n; ++k) {
+    bp[k] = reinterpret_cast<const uint8_t*>(b[k].data());
+    mp[k] = reinterpret_cast<int32_t*>(m[k].data());
+    dp[k] = reinterpret_cast<uint8_t*>(d[k].data());
+    bs[k] = ds[k] = (size_t)C[k] * 3;
+    ms[k] = (size_t)C[k] * 4;
+  }
+  const int rc = msg_watershed_colorize_batch(c, n, bp.data(), bs.data(), mp.data(), ms.data(), R.data(), C.data(),
+                                              depth, palette ? reinterpret_cast<const uint8_t*>(p.data()) : nullptr,
+                                              dp.data(), ds.data());
+  if (rc) return rc;
+  for (jsize k = 0; k < n; ++k) {
+    const long long nk = (long long)R[k] * C[k];
+    jintArray mk = static_cast<jintArray>(env->GetObjectArrayElement(markers, k));
+    jbyteArray dk = static_cast<jbyteArray>(env->GetObjectArrayElement(dsts, k));
+    env->SetIntArrayRegion(mk, 0, (jsize)nk, m[k].data());
+    env->SetByteArrayRegion(dk, 0, (jsize)(3 * nk), d[k].data());
+    env->DeleteLocalRef(mk);
+    env->DeleteLocalRef(dk);
+  }
+  return env->ExceptionCheck() ? MSG_EINVAL : MSG_OK;
+}
+
 // notConnectedMarkers' marker stage (PictureService.java:476-828): markers out, levels as
 // {start, end, count} triples into levelsOut (3 * 256 ints).  Returns the level count or a
 // negative MSG_E* code.

@@ -154,6 +154,74 @@ public final class MSegmentNative {
         return markers;
     }
 
+    /** msg_set_batch_floods: 0 the full engine per flood, 1 / 2 many floods per launch. */
+    private static native int setBatchFloods(long ctx, int mode);
+
+    /** Returns 0 or a negative MSG_E* code; every markers[k] rewritten in place, every dsts[k] filled. */
+    private static native int watershedColorizeBatch(long ctx, byte[][] bgrs, int[][] markers, int[] rows,
+                                                     int[] cols, int depth, byte[] paletteOrNull, byte[][] dsts);
+
+    private static final ThreadLocal<int[]> BATCH_MODE = ThreadLocal.withInitial(() -> new int[]{0});
+
+    /**
+     * PictureService.watershed over many frames in one native call: the reference's evaluation
+     * loop floods 92 frames per image (CorrelationTestService.java:84-86, 116, 128, 141, each through
+     * PictureService.watershed at :852).  manyFloods = true selects msg_set_batch_floods mode 1
+     * (every flood popped serially to its end, one wave per flood, all in one kernel: the mode for
+     * notConnectedMarkers' scattered seeds); false, the full engine per flood.  Labels are written
+     * back into each markers Mat, and the colourised frames are returned in order.  One palette
+     * (or null: colored = false) serves every frame, as one generateBGRColor draw per call would.
+     */
+    public static java.util.List<Mat> watershedBatch(java.util.List<Mat> srcs, java.util.List<Mat> markers,
+                                                     int depth, byte[] paletteOrNull, boolean manyFloods) {
+        int n = srcs.size();
+        if (markers.size() != n) {
+            throw new CvException("watershedBatch: " + n + " images but " + markers.size() + " marker maps");
+        }
+        byte[][] bgr = new byte[n][];
+        int[][] lab = new int[n][];
+        byte[][] out = new byte[n][];
+        int[] rows = new int[n];
+        int[] cols = new int[n];
+        for (int k = 0; k < n; k++) {
+            Mat src = srcs.get(k);
+            Mat mk = markers.get(k);
+            if (src.type() != CvType.CV_8UC3 || mk.type() != CvType.CV_32SC1 || !src.size().equals(mk.size())) {
+                throw new CvException("watershedBatch: frame " + k + ": src must be CV_8UC3 and markers CV_32SC1 "
+                        + "of the same size");
+            }
+            rows[k] = src.rows();
+            cols[k] = src.cols();
+            bgr[k] = new byte[rows[k] * cols[k] * 3];
+            lab[k] = new int[rows[k] * cols[k]];
+            out[k] = new byte[rows[k] * cols[k] * 3];
+            src.get(0, 0, bgr[k]);
+            mk.get(0, 0, lab[k]);
+        }
+        long ctx = CTX.get();
+        int mode = manyFloods ? 1 : 0;
+        int[] cur = BATCH_MODE.get();
+        if (cur[0] != mode) {  // switching back to 0 releases the mode's per-frame workspaces
+            int rc = setBatchFloods(ctx, mode);
+            if (rc != 0) {
+                throw new CvException("libmsegment error " + rc + ": " + lastError(ctx));
+            }
+            cur[0] = mode;
+        }
+        int rc = watershedColorizeBatch(ctx, bgr, lab, rows, cols, depth, paletteOrNull, out);
+        if (rc != 0) {
+            throw new CvException("libmsegment error " + rc + ": " + lastError(ctx));
+        }
+        java.util.List<Mat> dsts = new java.util.ArrayList<>(n);
+        for (int k = 0; k < n; k++) {
+            markers.get(k).put(0, 0, lab[k]);
+            Mat dst = new Mat(markers.get(k).size(), CvType.CV_8UC3);
+            dst.put(0, 0, out[k]);
+            dsts.add(dst);
+        }
+        return dsts;
+    }
+
     /** Drop-in for PictureService.watershed(src, markers, depth, colored) given its palette. */
     public static Mat watershed(Mat src, Mat markers, int depth, byte[] paletteOrNull) {
         if (src.type() != CvType.CV_8UC3 || markers.type() != CvType.CV_32SC1

@@ -185,8 +185,10 @@ class Segmenter:
                                          _vp(dst), W * 3))
         return dst
 
-    def watershed_batch(self, frames):
-        """frames: list of (bgr, markers); every markers array is rewritten in place."""
+    def watershed_batch(self, frames, depth=None, palette=None):
+        """frames: list of (bgr, markers); every markers array is rewritten in place.  With a
+        depth, also each frame's colorByIndexes (msg_watershed_colorize_batch): returns the list of
+        colourised BGR frames (palette: depth x 3 BGR bytes, None = white)."""
         n = len(frames)
         keep = []
         bp = (ctypes.c_void_p * n)()
@@ -205,7 +207,18 @@ class Segmenter:
             mp[k] = m.ctypes.data
             ms[k] = m.shape[1] * 4
             rows[k], cols[k] = m.shape
-        self._check(self._L.msg_watershed_batch(self._h, n, bp, bs, mp, ms, rows, cols))
+        if depth is None:
+            self._check(self._L.msg_watershed_batch(self._h, n, bp, bs, mp, ms, rows, cols))
+            return None
+        dsts = [np.empty(m.shape + (3,), np.uint8) for _, m in frames]
+        dp = (ctypes.c_void_p * n)(*[d.ctypes.data for d in dsts])
+        ds = (ctypes.c_size_t * n)(*[d.shape[1] * 3 for d in dsts])
+        pal = None
+        if palette is not None:
+            pal = np.ascontiguousarray(palette, dtype=np.uint8)
+        self._check(self._L.msg_watershed_colorize_batch(self._h, n, bp, bs, mp, ms, rows, cols, int(depth),
+                                                          pal.ctypes.data if pal is not None else None, dp, ds))
+        return dsts
 
     def set_batch_inflight(self, k):
         """Floods kept in flight by the batch calls (1..8; 1 = back to back)."""

@@ -35,7 +35,7 @@ def MSG_NC_MASK(k):
 # every symbol include/msegment.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "msg_create", "msg_destroy", "msg_last_error", "msg_abi_version", "msg_build_id", "msg_get_stats",
-    "msg_watershed", "msg_colorize", "msg_watershed_colorize", "msg_watershed_batch",
+    "msg_watershed", "msg_colorize", "msg_watershed_colorize", "msg_watershed_batch", "msg_watershed_colorize_batch",
     "msg_watershed_dev", "msg_colorize_dev", "msg_watershed_colorize_dev", "msg_edge_weights_dev",
     "msg_set_profiling", "msg_get_kernel_profile", "msg_set_diag", "msg_set_speculative",
     "msg_set_fast_commit",
@@ -150,6 +150,8 @@ def load():
     L.msg_watershed_colorize.restype = i
     L.msg_watershed_batch.argtypes = [vp, i, vp, vp, vp, vp, vp, vp]
     L.msg_watershed_batch.restype = i
+    L.msg_watershed_colorize_batch.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, i, vp, vp, vp]
+    L.msg_watershed_colorize_batch.restype = i
     L.msg_watershed_dev.argtypes = [vp, vp, vp, vp, i, i, vp]
     L.msg_watershed_dev.restype = i
     L.msg_colorize_dev.argtypes = [vp, vp, i, i, i, vp, vp, vp, vp]

@@ -36,10 +36,11 @@ def main():
         n = max(1, d[0])
         tot = max(1, d[2] + d[3] + d[4])
         print("%s: gens %d rounds %d execs/pop %.2f (replayed %.2f) | cascade pops (lane sums) %d, avg queue %.2f | cycles per cascade pop:"
-              " select %.0f (%.0f%%), loads %.0f (%.0f%%), writes %.0f (%.0f%%)" % (
+              " select %.0f (%.0f%%), loads %.0f (%.0f%%), writes %.0f (%.0f%%) | wave-cooperative pops %d, %.0f cycles each" % (
                   nm, st["spec_generations"], st["spec_rounds"], st["spec_executions"] / max(1, st["pops"]),
                   st["spec_replays"] / max(1, st["pops"]), d[0],
-                  d[1] / n, d[2] / n, 100.0 * d[2] / tot, d[3] / n, 100.0 * d[3] / tot, d[4] / n, 100.0 * d[4] / tot),
+                  d[1] / n, d[2] / n, 100.0 * d[2] / tot, d[3] / n, 100.0 * d[3] / tot, d[4] / n, 100.0 * d[4] / tot,
+                  d[5], d[6] / max(1, d[5])),
               flush=True)
         # wall-clock split of the round kernels (diag bank 1, 10 ns ticks): wave time in top-pop
         # waits / cascades / whole kernel, and the sum over rounds of each round's longest wave

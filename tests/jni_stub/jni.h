@@ -23,12 +23,14 @@ class _jstring : public _jobject {};
 class _jarray : public _jobject {};
 class _jbyteArray : public _jarray {};
 class _jintArray : public _jarray {};
+class _jobjectArray : public _jarray {};
 typedef _jobject* jobject;
 typedef _jclass* jclass;
 typedef _jstring* jstring;
 typedef _jarray* jarray;
 typedef _jbyteArray* jbyteArray;
 typedef _jintArray* jintArray;
+typedef _jobjectArray* jobjectArray;
 
 struct JNIEnv_ {
   jsize GetArrayLength(jarray array);
@@ -40,6 +42,8 @@ struct JNIEnv_ {
   jboolean ExceptionCheck();
   void* GetPrimitiveArrayCritical(jarray array, jboolean* isCopy);
   void ReleasePrimitiveArrayCritical(jarray array, void* carray, jint mode);
+  jobject GetObjectArrayElement(jobjectArray array, jsize index);
+  void DeleteLocalRef(jobject obj);
 };
 typedef JNIEnv_ JNIEnv;
 #endif

@@ -4,6 +4,7 @@
 // the shim never holds one across a library call.
 //   mock_env validate            -- argument checks only (no GPU): every bad call -> MSG_EINVAL
 //   mock_env run <in> <out>      -- one watershedColorize through the shim on GPU 0
+//   mock_env batch <mode> <in> <out> -- watershedColorizeBatch of the frames in <in> (batch floods mode)
 #include <jni.h>
 
 #include <cstdio>
@@ -24,6 +25,9 @@ jint Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_shapeMarkers(JNI
                                                                              jbyteArray, jint, jint, jintArray);
 jint Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_colorMarkers(JNIEnv*, jclass, jlong, jbyteArray,
                                                                              jint, jint, jbyteArray, jintArray);
+jint Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_setBatchFloods(JNIEnv*, jclass, jlong, jint);
+jint Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_watershedColorizeBatch(
+    JNIEnv*, jclass, jlong, jobjectArray, jobjectArray, jintArray, jintArray, jint, jbyteArray, jobjectArray);
 }
 
 struct Bytes : _jbyteArray {
@@ -33,6 +37,9 @@ struct Bytes : _jbyteArray {
 struct Ints : _jintArray {
   std::vector<jint> v;
   explicit Ints(size_t n) : v(n) {}
+};
+struct Objs : _jobjectArray {
+  std::vector<jobject> v;
 };
 
 static bool g_exc = false;
@@ -72,6 +79,19 @@ void* JNIEnv_::GetPrimitiveArrayCritical(jarray, jboolean*) {
   return nullptr;
 }
 void JNIEnv_::ReleasePrimitiveArrayCritical(jarray, void*, jint) {}
+static int g_refs = 0;  // local references handed out and not deleted
+jobject JNIEnv_::GetObjectArrayElement(jobjectArray a, jsize i) {
+  Objs* o = static_cast<Objs*>(a);
+  if (i < 0 || (size_t)i >= o->v.size()) {
+    g_exc = true;
+    return nullptr;
+  }
+  if (o->v[i]) ++g_refs;
+  return o->v[i];
+}
+void JNIEnv_::DeleteLocalRef(jobject r) {
+  if (r) --g_refs;
+}
 
 static Bytes* bytes(size_t n) {
   Bytes* b = new Bytes(n);
@@ -81,6 +101,17 @@ static Bytes* bytes(size_t n) {
 static Ints* ints(size_t n) {
   Ints* a = new Ints(n);
   reg(static_cast<jarray>(a), n);
+  return a;
+}
+static Objs* objs(std::vector<jobject> v) {
+  Objs* o = new Objs;
+  o->v = std::move(v);
+  reg(static_cast<jarray>(o), o->v.size());
+  return o;
+}
+static Ints* ints_of(std::vector<jint> v) {
+  Ints* a = ints(v.size());
+  a->v = std::move(v);
   return a;
 }
 
@@ -123,8 +154,43 @@ static int validate() {
              &env, nullptr, fake, bytes(3 * N), R, C, bytes(3 * N - 1), ints(N)), "color short sharp");
   expect(Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_colorMarkers(
              &env, nullptr, fake, bytes(3 * N), R, C, bytes(3 * N), ints(N - 1)), "color short markers");
+  // the batch entry: mismatched array counts, a short frame array, a negative depth
+  auto batch = [&](jlong cx, Objs* b, Objs* m, Ints* r, Ints* c, jint depth, Bytes* pal, Objs* d) {
+    return Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_watershedColorizeBatch(&env, nullptr, cx, b, m, r,
+                                                                                             c, depth, pal, d);
+  };
+  auto frames = [&](int n, size_t nb, size_t nm, size_t nd) {
+    std::vector<jobject> b, m, d;
+    for (int k = 0; k < n; ++k) {
+      b.push_back(bytes(nb));
+      m.push_back(ints(nm));
+      d.push_back(bytes(nd));
+    }
+    return std::vector<Objs*>{objs(b), objs(m), objs(d)};
+  };
+  {
+    auto f = frames(2, 3 * N, N, 3 * N);
+    expect(batch(0, f[0], f[1], ints_of({R, R}), ints_of({C, C}), 2, nullptr, f[2]), "batch null ctx");
+    expect(batch(fake, f[0], f[1], ints_of({R}), ints_of({C, C}), 2, nullptr, f[2]), "batch short rows");
+    expect(batch(fake, f[0], f[1], ints_of({R, R}), ints_of({C, C}), -1, nullptr, f[2]), "batch negative depth");
+    expect(batch(fake, f[0], f[1], ints_of({R, R}), ints_of({C, C}), 4, bytes(11), f[2]), "batch short palette");
+    auto g = frames(3, 3 * N, N, 3 * N);
+    expect(batch(fake, f[0], g[1], ints_of({R, R}), ints_of({C, C}), 2, nullptr, f[2]), "batch count mismatch");
+    auto h = frames(2, 3 * N, N - 1, 3 * N);
+    expect(batch(fake, h[0], h[1], ints_of({R, R}), ints_of({C, C}), 2, nullptr, h[2]), "batch short markers");
+    auto e = frames(2, 3 * N, N, 3 * N - 1);
+    expect(batch(fake, e[0], e[1], ints_of({R, R}), ints_of({C, C}), 2, nullptr, e[2]), "batch short dst");
+    Objs* holes = objs({bytes(3 * N), nullptr});
+    expect(batch(fake, holes, f[1], ints_of({R, R}), ints_of({C, C}), 2, nullptr, f[2]), "batch null frame");
+  }
+  expect(Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_setBatchFloods(&env, nullptr, 0, 1),
+         "batch floods null ctx");
   if (g_critical) {
     std::printf("FAIL critical regions taken: %d\n", g_critical);
+    ++bad;
+  }
+  if (g_refs) {
+    std::printf("FAIL local references leaked: %d\n", g_refs);
     ++bad;
   }
   std::printf("%s (%d bad)\n", bad ? "validate FAILED" : "validate ok", bad);
@@ -162,9 +228,59 @@ static int run(const char* in, const char* out) {
   return (g_critical || g_exc) ? 4 : 0;
 }
 
+// in: int32 n, depth, has_palette; [depth*3 palette bytes]; n x {int32 rows, cols; BGR bytes;
+// int32 markers}.  out: rc, then per frame the markers and the dst bytes.
+static int run_batch(int mode, const char* in, const char* out) {
+  FILE* f = std::fopen(in, "rb");
+  if (!f) return 2;
+  int32_t hdr[3];
+  if (std::fread(hdr, 4, 3, f) != 3) return 2;
+  const int n = hdr[0], depth = hdr[1];
+  Bytes* pal = hdr[2] ? bytes(3 * (size_t)depth) : nullptr;
+  if (pal && std::fread(pal->v.data(), 1, 3 * (size_t)depth, f) != 3 * (size_t)depth) return 2;
+  std::vector<jobject> b, m, d;
+  std::vector<jint> rv, cv;
+  for (int k = 0; k < n; ++k) {
+    int32_t rc2[2];
+    if (std::fread(rc2, 4, 2, f) != 2) return 2;
+    const size_t N = (size_t)rc2[0] * rc2[1];
+    Bytes* bk = bytes(3 * N);
+    Ints* mk = ints(N);
+    if (std::fread(bk->v.data(), 1, 3 * N, f) != 3 * N || std::fread(mk->v.data(), 4, N, f) != N) return 2;
+    b.push_back(bk);
+    m.push_back(mk);
+    d.push_back(bytes(3 * N));
+    rv.push_back(rc2[0]);
+    cv.push_back(rc2[1]);
+  }
+  std::fclose(f);
+  msg_ctx* c = nullptr;
+  if (msg_create(&c, 0, 0) != MSG_OK) return 3;
+  JNIEnv env;
+  const jlong cx = reinterpret_cast<jlong>(c);
+  jint rc = Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_setBatchFloods(&env, nullptr, cx, mode);
+  Objs* ob = objs(b);
+  Objs* om = objs(m);
+  Objs* od = objs(d);
+  if (rc == MSG_OK)
+    rc = Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_watershedColorizeBatch(
+        &env, nullptr, cx, ob, om, ints_of(rv), ints_of(cv), depth, pal, od);
+  msg_destroy(c);
+  FILE* g = std::fopen(out, "wb");
+  std::fwrite(&rc, 4, 1, g);
+  for (int k = 0; k < n; ++k) {
+    std::fwrite(static_cast<Ints*>(m[k])->v.data(), 4, static_cast<Ints*>(m[k])->v.size(), g);
+    std::fwrite(static_cast<Bytes*>(d[k])->v.data(), 1, static_cast<Bytes*>(d[k])->v.size(), g);
+  }
+  std::fclose(g);
+  std::printf("batch rc=%d critical=%d exc=%d refs=%d\n", rc, g_critical, (int)g_exc, g_refs);
+  return (g_critical || g_exc || g_refs) ? 4 : 0;
+}
+
 int main(int argc, char** argv) {
   if (argc >= 2 && std::string(argv[1]) == "validate") return validate();
   if (argc >= 4 && std::string(argv[1]) == "run") return run(argv[2], argv[3]);
-  std::fprintf(stderr, "usage: mock_env validate | run <in> <out>\n");
+  if (argc >= 5 && std::string(argv[1]) == "batch") return run_batch(std::atoi(argv[2]), argv[3], argv[4]);
+  std::fprintf(stderr, "usage: mock_env validate | run <in> <out> | batch <mode> <in> <out>\n");
   return 2;
 }

@@ -61,3 +61,46 @@ def test_jni_shim_watershed_on_gpu(tmp_path):
     want = ws_oracle.watershed(img, m)
     assert np.array_equal(lab, want)
     assert np.array_equal(out, ws_oracle.colorize(want, d, pal))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+def test_jni_shim_batch_on_gpu(tmp_path, mode):
+    """MSegmentNative.watershedColorizeBatch through the shim: CorrelationTestService's many floods
+    per image (CorrelationTestService.java:84-86, 141 -> PictureService.java:852) handed over in one
+    call, in the default batch path (mode 0) and the many-floods mode (mode 1)."""
+    from msegment import synth
+    from msegment.jrandom import generate_bgr_palette
+    from oracle import ws_oracle
+
+    exe = build(tmp_path)
+    rng = np.random.default_rng(11)
+    frames = []
+    for k, (H, W) in enumerate(((96, 128), (64, 64), (0, 7), (130, 70), (33, 41))):
+        img = synth.frame("mosaic_noise", max(H, 1), max(W, 1), 20 + k)[0][:H, :W]
+        m = np.where(rng.random((H, W)) < 0.03, rng.integers(1, 6, (H, W)), 0).astype(np.int32)
+        frames.append((np.ascontiguousarray(img), m))
+    depth = 5
+    pal = generate_bgr_palette(depth, 3)
+    src, dst = str(tmp_path / "in.bin"), str(tmp_path / "out.bin")
+    with open(src, "wb") as f:
+        f.write(struct.pack("<3i", len(frames), depth, 1))
+        f.write(np.ascontiguousarray(pal, dtype=np.uint8).tobytes())
+        for img, m in frames:
+            f.write(struct.pack("<2i", *m.shape))
+            f.write(img.tobytes())
+            f.write(m.tobytes())
+    r = subprocess.run([exe, "batch", str(mode), src, dst], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    raw = open(dst, "rb").read()
+    assert struct.unpack("<i", raw[:4])[0] == 0
+    off = 4
+    for img, m in frames:
+        n = m.size
+        lab = np.frombuffer(raw[off:off + 4 * n], np.int32).reshape(m.shape)
+        off += 4 * n
+        out = np.frombuffer(raw[off:off + 3 * n], np.uint8).reshape(m.shape + (3,))
+        off += 3 * n
+        want = ws_oracle.watershed(img, m)
+        assert np.array_equal(lab, want)
+        assert np.array_equal(out, ws_oracle.colorize(want, depth, pal))
