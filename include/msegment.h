@@ -63,8 +63,8 @@ typedef struct msg_stats {
                                dependency-loop cycles, loop rounds, max loop cycles, wave-rounds;
                                small-batch loop rounds, small-batch loop entries; reserved.
                                When speculative generations ran (10 ns ticks): sums over the
-                               rounds of the round's longest wave's dealing + promotion and of
-                               its log copy + change marks; wave time in the round kernel;
+                               rounds of the round's longest wave's wave-cooperative cascades
+                               and of its log copy + change marks; wave time in the round kernel;
                                longest wave; sums over the rounds of the longest wave's top-pop
                                waits, of its whole time, of its top-pop writes + cascades; waves */
     /* speculative generations (the interrupt-dense regime; msg_set_speculative) */

@@ -84,7 +84,7 @@ struct msg_ctx {
   bool prof = false;
   unsigned long long* d_diag = nullptr;  // 8 counters when diagnostics are on
   bool diag = false;
-  int diag_bank = 0;  // msg_set_diag(ctx, 3): report the small-batch loop's regime split (bank 2)
+  int diag_bank = 0;  // msg_set_diag(ctx, 3 / 4): report bank 2 (the small-batch loop's regime split) / 3
   int inject = 0;  // msg_set_diag(ctx, 2): k_resolve give-up injection (tests)
   std::vector<hipEvent_t> evpool;
   size_t evused = 0;
@@ -477,7 +477,7 @@ int flood_begin(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int H,
   const int gsc = std::min(npx * (CH / 1024), 1024);
   HIPCHK(c, hipMemsetAsync(c->d_ctl, 0, sizeof(Ctl), st));
   HIPCHK(c, hipMemsetAsync(c->d_capp, 0, (size_t)CAP_SLOTS * NQ * 4, st));
-  if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 24 * sizeof(unsigned long long), st));
+  if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 32 * sizeof(unsigned long long), st));
   HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)npx * NQ * sizeof(int32_t), st));
   const int nrc = H * ws.nseg;  // raster chunks
   // k_prep4 (one thread per tile) where widths and buffers allow 12-B / 16-B quad loads
@@ -597,7 +597,7 @@ int flood_end(msg_ctx* c, FloodRun& fr, int32_t* d_labels, int depth = 0, const 
   }
   Ctl tail;
   HIPCHK(c, hipMemcpyAsync(&tail, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
-  unsigned long long dgv[24] = {0};
+  unsigned long long dgv[32] = {0};
   if (c->diag) HIPCHK(c, hipMemcpyAsync(dgv, c->d_diag, sizeof(dgv), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
   c->stats.host_syncs += 1;
@@ -618,7 +618,7 @@ int flood_end(msg_ctx* c, FloodRun& fr, int32_t* d_labels, int depth = 0, const 
 #ifdef MSEG_CF_PROF
     c->stats.diag[k] = (int64_t)dgv[8 + k];  // k_commit_fast's phase split (diagnostic build)
 #else
-    c->stats.diag[k] = (int64_t)dgv[c->diag_bank == 2 ? 16 + k : tail.spec.gens ? 8 + k : k];
+    c->stats.diag[k] = (int64_t)dgv[c->diag_bank >= 2 ? 8 * c->diag_bank + k : tail.spec.gens ? 8 + k : k];
 #endif
   c->stats.spec_generations = tail.spec.gens;
   c->stats.spec_rounds = tail.spec.rounds_total;
@@ -1185,11 +1185,11 @@ int msg_set_diag(msg_ctx* c, int enable) {
   if (!c) return MSG_EINVAL;
   if (enable && !c->d_diag) {
     HIPCHK(c, hipSetDevice(c->dev));
-    HIPCHK(c, hipMalloc((void**)&c->d_diag, 24 * sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc((void**)&c->d_diag, 32 * sizeof(unsigned long long)));
   }
   c->diag = enable != 0;
   c->inject = enable == 2;
-  c->diag_bank = enable == 3 ? 2 : 0;
+  c->diag_bank = enable == 3 ? 2 : enable == 4 ? 3 : 0;
   return MSG_OK;
 }
 

@@ -158,6 +158,35 @@ __device__ __forceinline__ int spec_decide(const SpecView& V, const SpecRec& r, 
   return (r.s >= WSHED) ? r.s : INQ;
 }
 
+// a value per lane from five wave-uniform ones (lane 0: a0, ... lane 3: a3, others a4), as
+// sequential selects (a chain of conditional expressions compiled to a branch tree)
+__device__ __forceinline__ int lane_pick(int lane, int a0, int a1, int a2, int a3, int a4) {
+  int r = a4;
+  r = (lane == 3) ? a3 : r;
+  r = (lane == 2) ? a2 : r;
+  r = (lane == 1) ? a1 : r;
+  r = (lane == 0) ? a0 : r;
+  return r;
+}
+
+// spec_decide for an own view, as selects only (the cooperative pops run it on four lanes; its
+// early returns compiled to a tree of exec-masked branches there)
+__device__ __forceinline__ int spec_decide_own(const SpecView& V, const SpecRec& r, int j) {
+  const unsigned long long o = V.par ? r.cl1 : r.cl0;
+  const int lc = (int)(uint32_t)(V.par ? (r.labs >> 32) : r.labs);
+  const unsigned long long f = r.fin;
+  const unsigned long long c = V.par ? r.cl0 : r.cl1;
+  const int lp = (int)(uint32_t)(V.par ? r.labs : (r.labs >> 32));
+  const bool c1 = (sc_tag(o) == V.T) & (sc_rank(o) == j);  // (no short-circuit: no branches)
+  const bool c2 = (unsigned)(f >> 33) == V.G;
+  const bool c3 = V.hasprev & (sc_tag(c) == V.T - 1) & (sc_rank(c) < j);
+  const int v1 = (o & 1ull) ? lc : INQ;
+  const int v2 = ((f >> 32) & 1ull) ? (int)(uint32_t)f : INQ;
+  const int v3 = (c & 1ull) ? lp : INQ;
+  const int v4 = (r.s >= WSHED) ? r.s : INQ;
+  return c1 ? v1 : c2 ? v2 : c3 ? v3 : v4;
+}
+
 // top-pop granule of item k as item j may use it in round T: this round's, or a final item's.
 // Word: label | round tag << 32 | (label differs from item k's previous round) << 63; chg
 // collects that bit of the non-final items read (an input of the reader changed).
@@ -210,7 +239,7 @@ __device__ void spec_finalize(Ctl* ctl, int P, int n, unsigned T, unsigned G, un
     dg[4] += (k >> 20) & 0xfffffu; // its waits for earlier items' top pops
     dg[6] += k & 0xfffffu;         // its top-pop writes + cascades
     const unsigned long long k2 = __hip_atomic_load(&s.rmax2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    dg[0] += (k2 >> 20) & 0xfffffu;  // its dealing + promotion of final items' claims
+    dg[0] += (k2 >> 20) & 0xfffffu;  // its cascades run wave-cooperatively (spec_coop)
     dg[1] += k2 & 0xfffffu;          // its log copy, change marks, candidates
     s.rmax = 0;
     s.rmax2 = 0;
@@ -274,6 +303,7 @@ __device__ void spec_finalize(Ctl* ctl, int P, int n, unsigned T, unsigned G, un
 // The execution's results (records, signature, overflow flags, record chunks) land where the
 // per-lane loop leaves them, so the rest of the round does not know which form ran it.
 constexpr int COOP_HOT = SPEC_QCAP * 64;  // hot slots of a cooperating wave (its LDS columns)
+constexpr int COOP_LANES = 2;             // the wave takes cascades over once this few lanes are left
 constexpr int COOP_MAXORD = 0x7fffffff;
 static_assert(4 * SPEC_MAXREC < (1 << 16), "an execution's push sequence fits the 16 bits of a coop ord");
 
@@ -441,10 +471,33 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
       }
     }
   };
+  // the previous pop's claims (lane 0 its pixel, lanes 1-4 its pushes), label and record, one
+  // masked instruction each
+  auto coop_writes = [&]() {
+    const int za = lane_pick(lane, S.py, S.pz0, S.pz1, S.pz2, S.pz3);
+    const bool cl = lane == 0 || (lane <= 4 && ((S.ppm >> ((lane - 1) & 3)) & 1u));
+    const unsigned long long cv = spec_claim(T, j, lane == 0 ? 1u : 0u);
+    if (cl) claim_max(&spx[za].cl[par], cv);
+    if (lane == 5) st_ag32(&spx[S.py].lab[par], S.plab);
+    if (lane == 6) *rec_at(S.nrec - 1) = S.prec;
+    S.pwrite = false;
+  };
   int y = S.y;
 #ifdef MSEG_SPEC_PROF
   const long long c_t0 = (long long)__builtin_amdgcn_s_memtime();
   const int c_n0 = S.nrec;
+  // bank 3 (msg_set_diag 4): cycles of a cooperative pop by phase -- loads issued + hole fixed,
+  // the wait for the loads, the previous pop's writes, decide, pushes + record, select
+  long long c_ph[6] = {0, 0, 0, 0, 0, 0};
+  long long c_tq = 0;
+  auto c_mark = [&](int k) {
+    const long long t = (long long)__builtin_amdgcn_s_memtime();
+    c_ph[k] += t - c_tq;
+    c_tq = t;
+  };
+#define COOP_MARK(k) c_mark(k)
+#else
+#define COOP_MARK(k) (void)0
 #endif
   for (;;) {
     // ---- the length caps and the record chunk of pop nrec, as at the per-lane loop's head ----
@@ -465,21 +518,25 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
       else S.xb3 = b;
     }
     // ---- the pop of y: its loads (lanes 0-3 one neighbour each), then the previous pop's writes ----
+#ifdef MSEG_SPEC_PROF
+    c_tq = (long long)__builtin_amdgcn_s_memtime();
+#endif
     const int yb = y + marg;
-    const int nbd = nbi(yb, lane & 3, Wt) - marg;
-    SpecRec r;
-    unsigned wyl = 0;
-    if (lane < 4) {
-      wyl = (unsigned)ws.w4[y];
-      r = spec_load(ws, V, nbd);
-    }
+    int nb[4];  // uniform: scalar arithmetic, then one lane per direction
+#pragma unroll
+    for (int d = 0; d < 4; ++d) nb[d] = __builtin_amdgcn_readfirstlane(nbi(yb, d, Wt) - marg);
+    const int nbd = lane_pick(lane, nb[0], nb[1], nb[2], nb[3], nb[3]);  // lane d: direction d
+    // every lane loads (lanes 4-63 repeat lane 3's addresses: the same requests), so that no
+    // branch puts the use of the loaded values -- and the wait for them -- before the hole fix
+    const unsigned wyl = (unsigned)ws.w4[y];
+    const SpecRec r = spec_load(ws, V, nbd);
     if (fix >= 0) {  // the column the last select popped from: fill its hole, find its new minimum
-      if (lane == fix) {
+      if (lane == fix) {  // the last entry moves into the hole (itself when it was the last)
         --cnt;
-        if (m1row != cnt) col[(size_t)m1row * SPEC_BS] = col[(size_t)cnt * SPEC_BS];
+        col[(size_t)m1row * SPEC_BS] = col[(size_t)cnt * SPEC_BS];
       }
       const int co = __builtin_amdgcn_readlane(cnt, fix);
-      const unsigned long long x = (lane < co) ? lq[(size_t)lane * SPEC_BS + wb + fix] : 0ull;
+      const unsigned long long x = lq[(size_t)(lane & (SPEC_QCAP - 1)) * SPEC_BS + wb + fix];
       const int ord = (lane < co) ? (int)(x >> 32) : COOP_MAXORD;
       const int mo = wave_min(ord);
       const unsigned long long bo = __ballot(lane < co && ord == mo);
@@ -492,32 +549,24 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
       }
       fix = -1;
     }
+    COOP_MARK(0);
     vm_drain();
-    if (S.pwrite) {  // claims of the previous pop, its label and its record: one instruction each
-      const int d = lane - 2;
-      const int zl = d == 0 ? S.pz0 : d == 1 ? S.pz1 : d == 2 ? S.pz2 : S.pz3;
-      if (lane == 0) claim_max(&spx[S.py].cl[par], spec_claim(T, j, 1u));
-      else if (d >= 0 && d < 4 && ((S.ppm >> d) & 1u)) claim_max(&spx[zl].cl[par], spec_claim(T, j, 0u));
-      if (lane == 1) st_ag32(&spx[S.py].lab[par], S.plab);
-      if (lane == 6) *rec_at(S.nrec - 1) = S.prec;
-      S.pwrite = false;
-    }
+    COOP_MARK(1);
+    if (S.pwrite) coop_writes();
+    COOP_MARK(2);
     // ---- decide: lanes 0-3, patched with the previous pop's writes (issued after these loads) ----
     int v = 0;
-    if (lane < 4) {
-      v = spec_decide(V, r, j, true);
-      if (nbd == S.py) v = S.plab;
-      if (((S.ppm & 1u) && nbd == S.pz0) || ((S.ppm & 2u) && nbd == S.pz1) || ((S.ppm & 4u) && nbd == S.pz2) ||
-          ((S.ppm & 8u) && nbd == S.pz3))
-        v = INQ;
+    {
+      v = spec_decide_own(V, r, j);
+      v = (nbd == S.py) ? S.plab : v;
+      const bool inq = (((S.ppm & 1u) != 0) & (nbd == S.pz0)) | (((S.ppm & 2u) != 0) & (nbd == S.pz1)) |
+                       (((S.ppm & 4u) != 0) & (nbd == S.pz2)) | (((S.ppm & 8u) != 0) & (nbd == S.pz3));
+      v = inq ? INQ : v;
     }
     const unsigned wy = (unsigned)__builtin_amdgcn_readfirstlane((int)wyl);
-    int vd[4], nb[4];
+    int vd[4];
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      vd[d] = __builtin_amdgcn_readlane(v, d);
-      nb[d] = __builtin_amdgcn_readlane(nbd, d);
-    }
+    for (int d = 0; d < 4; ++d) vd[d] = __builtin_amdgcn_readlane(v, d);
     int lab = 0;
 #pragma unroll
     for (int d = 0; d < 4; ++d)
@@ -526,6 +575,7 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
       S.ovf = true;
       lab = WSHED;
     }
+    COOP_MARK(3);
     unsigned dmy = 0, pmy = 0;
     if (lab != WSHED) {
 #pragma unroll
@@ -548,6 +598,7 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
     S.pz3 = nb[3];
     S.pwrite = true;
     ++S.nrec;
+    COOP_MARK(4);
     if (S.ovf || H + S.nc == 0) break;
     // ---- select: the smallest ord of all columns ----
     if (H == 0) {
@@ -558,21 +609,27 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
     fix = __builtin_ctzll(__ballot(m1 == m));
     y = __builtin_amdgcn_readlane(m1pix, fix);
     --H;
+    COOP_MARK(5);
+    // the loop-carried state is wave-uniform: say so, so that the loop's branches stay scalar
+    H = __builtin_amdgcn_readfirstlane(H);
+    rr = __builtin_amdgcn_readfirstlane(rr);
+    S.nrec = __builtin_amdgcn_readfirstlane(S.nrec);
+    S.nc = __builtin_amdgcn_readfirstlane(S.nc);
+    S.cb = __builtin_amdgcn_readfirstlane(S.cb);
+    S.cmin = (unsigned)__builtin_amdgcn_readfirstlane((int)S.cmin);
+    S.qseq = (unsigned)__builtin_amdgcn_readfirstlane((int)S.qseq);
+    S.ovf = __builtin_amdgcn_readfirstlane((int)S.ovf) != 0;
+    S.cap = __builtin_amdgcn_readfirstlane((int)S.cap) != 0;
   }
-  if (S.pwrite) {  // the last pop's writes
-    const int d = lane - 2;
-    const int zl = d == 0 ? S.pz0 : d == 1 ? S.pz1 : d == 2 ? S.pz2 : S.pz3;
-    if (lane == 0) claim_max(&spx[S.py].cl[par], spec_claim(T, j, 1u));
-    else if (d >= 0 && d < 4 && ((S.ppm >> d) & 1u)) claim_max(&spx[zl].cl[par], spec_claim(T, j, 0u));
-    if (lane == 1) st_ag32(&spx[S.py].lab[par], S.plab);
-    if (lane == 6) *rec_at(S.nrec - 1) = S.prec;
-    S.pwrite = false;
-  }
+  if (S.pwrite) coop_writes();  // the last pop's
 #ifdef MSEG_SPEC_PROF
-  if (ws.diag && lane == 0) {  // bank 2: cooperative pops, their cycles
+  if (ws.diag && lane == 0) {  // bank 2: cooperative pops, their cycles; bank 3: the phase split
     atomicAdd(&ws.diag[21], (unsigned long long)(S.nrec - c_n0));
     atomicAdd(&ws.diag[22], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - c_t0));
+#pragma unroll
+    for (int k = 0; k < 6; ++k) atomicAdd(&ws.diag[24 + k], (unsigned long long)c_ph[k]);
   }
+#undef COOP_MARK
 #endif
 }
 
@@ -617,7 +674,7 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
 #endif
   unsigned long long* const dg = ws.diag ? ws.diag + 8 : nullptr;  // msg_set_diag: the round's wall-clock split (10 ns ticks)
   const long long tk0 = dg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
-  long long tw = 0, tc = 0, tpr = 0, tpo = 0;  // diag: waits, cascades, dealing + promotion, post
+  long long tw = 0, tc = 0, tco = 0, tpo = 0;  // diag: waits, cascades (cooperative part), post
   __syncthreads();
   while (!stop) {
     const long long tq0 = dg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
@@ -643,7 +700,7 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
           if ((dm >> d) & 1u) st_ag64(&ws.spx[nbi(y + marg, d, Wt) - marg].fin, fin_word(G, 0u, 0));
       }
     }
-    if (dg) tpr += (long long)__builtin_amdgcn_s_memrealtime() - tq0;
+    (void)tq0;
     // ---- execute [P, n): gather the top pop ----
     const bool ex = j >= P && j < n;
     int p = 0;
@@ -1102,11 +1159,35 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
         pf_write += (long long)__builtin_amdgcn_s_memtime() - q4 + (q3 - q2);
 #endif
        }
-        // one lane left with a cascade: the wave takes it over (spec_coop) and finishes it
-        const unsigned long long bal = __ballot(more);
+        // at most COOP_LANES lanes left with cascades: the wave takes them over (spec_coop) and
+        // finishes them one after another; every one but the first first moves its hot keys to
+        // its cold chunk (the cooperative queue reuses the wave's LDS columns)
+        unsigned long long bal = __ballot(more);
         if (bal == 0) break;
-        if (__popcll(bal) == 1) {
-          const int w = __builtin_ctzll(bal);
+        if (__popcll(bal) <= COOP_LANES) {
+          const int w0 = __builtin_ctzll(bal);
+          const bool canspill = !more || lane == w0 || nq == 0 || (cb != -2 && nc + nq <= SPEC_CCAP);
+          if (!__all(canspill)) continue;  // (pool full: those lanes carry on alone)
+          if (more && lane != w0 && nq > 0) {
+            if (cb < 0 && (cb = pool_get(SPEC_CCAP)) < 0) {
+              cb = -2;
+              ovf = cap = true;  // a capacity overflow, as a failed cold push would be
+              more = false;
+            } else {
+              for (int e = 0; e < nq; ++e) {
+                const unsigned long long k = lq[(size_t)e * SPEC_BS + tid];
+                ws.sxp[(size_t)cb + nc + e] = k;
+                cmin = min(cmin, (unsigned)(k >> 52));
+              }
+              nc += nq;
+              nq = 0;
+              hmx = 0;
+            }
+          }
+          bal = __ballot(more);
+        }
+        if (bal != 0 && __popcll(bal) <= COOP_LANES) for (unsigned long long lb = bal; lb; lb &= lb - 1) {
+          const int w = __builtin_ctzll(lb);
           CoopSt S;
           S.y = __builtin_amdgcn_readlane(y, w);
           S.py = __builtin_amdgcn_readlane(py, w);
@@ -1133,8 +1214,10 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
           S.ovf = S.cap = false;
           const int jw = __builtin_amdgcn_readlane(j, w);
           const int wb = tid & ~63;
+          const long long tco0 = dg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
           spec_coop(ws, V, lq, wb, w, jw, L, jw == P || (lcap && T > G),
                     ws.stmp + (size_t)(blockIdx.x * SPEC_BS + wb + w) * SPEC_RL, S);
+          if (dg) tco += (long long)__builtin_amdgcn_s_memrealtime() - tco0;
           if (lane == w) {
             nrec = S.nrec;
             sig = S.sig;
@@ -1147,7 +1230,6 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
             nq = nc = 0;
             more = false;
           }
-          break;
         }
       }
     }  // the execution
@@ -1164,12 +1246,28 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
     if (lane == 0 && wtot) wbase = atomicAdd(&ctl->slogtop.v, wtot);
     wbase = __builtin_amdgcn_readlane(wbase, 0);
     int fcand = NONE, ocand = NONE;
+    // this lane's log copy, its marks of the new / the previous round's records: done per lane for
+    // short executions, by the whole wave (64 records per step, one execution at a time) for long
+    // ones -- a long cascade's records used to be copied and marked by its lane alone, record by
+    // record, on the round's critical path (~9% of uniform noise's round time, round 5)
+    constexpr int LONGREC = 16;
+    bool cpy = false, mkn = false, mkp = false;
+    int4 prv = make_int4(0, 0, 0, 0);
+    int base = 0;
+    unsigned* const dn = ws.sdirt + (size_t)par * ws.snp;
+    auto mark = [&](unsigned long long r) {
+      const int y = (int)(r & 0x0fffffffu);
+      const unsigned dmy = (unsigned)(r >> 28) & 15u;
+      dn[y] = T;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        if ((dmy >> d) & 1u) dn[nbi(y + marg, d, Wt) - marg] = T;
+    };
     if (ex) {
-      const int base = rbase >= 0 ? rbase : wbase + incl - want;
+      base = rbase >= 0 ? rbase : wbase + incl - want;
       if (!ovf && rbase < 0) {
         if ((long long)base + nrec > ws.slogcap) ovf = cap = true;  // generation log full
-        else
-          for (int k = 0; k < nrec; ++k) ws.slog[base + k] = *rec_at(k);
+        else cpy = true;
       }
       sig = smix(sig, ((unsigned long long)nrec << 1) | (ovf ? 1ull : 0ull));
       ws.srec[(size_t)par * SPEC_WIN + j] = make_int4(base, ovf ? 0 : nrec, (int)T, cap ? 1 : 0);
@@ -1182,20 +1280,36 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
       if (rbase >= 0) ++nrep;
       else nxpop += nrec;
       if (changed) {  // mark both executions' claims: round T + 1 replays nothing that viewed them
-        unsigned* const dn = ws.sdirt + (size_t)par * ws.snp;
-        auto mark = [&](unsigned long long r) {
-          const int y = (int)(r & 0x0fffffffu);
-          const unsigned dmy = (unsigned)(r >> 28) & 15u;
-          dn[y] = T;
-#pragma unroll
-          for (int d = 0; d < 4; ++d)
-            if ((dmy >> d) & 1u) dn[nbi(y + marg, d, Wt) - marg] = T;
-        };
-        if (rbase < 0)
-          for (int k = 0; k < nrec; ++k) mark(*rec_at(k));
-        const int4 pr = ws.srec[(size_t)ppar * SPEC_WIN + j];
-        if (V.hasprev && pr.z == (int)(T - 1u))
-          for (int k = 0; k < pr.y; ++k) mark(ws.slog[pr.x + k]);
+        mkn = rbase < 0;
+        prv = ws.srec[(size_t)ppar * SPEC_WIN + j];
+        mkp = V.hasprev && prv.z == (int)(T - 1u) && prv.y > 0;
+      }
+      if (cpy && nrec <= LONGREC)
+        for (int k = 0; k < nrec; ++k) ws.slog[base + k] = *rec_at(k);
+      if (mkn && nrec <= LONGREC)
+        for (int k = 0; k < nrec; ++k) mark(*rec_at(k));
+      if (mkp && prv.y <= LONGREC)
+        for (int k = 0; k < prv.y; ++k) mark(ws.slog[prv.x + k]);
+    }
+    {
+      const int wb = tid & ~63;
+      for (unsigned long long lb = __ballot((cpy || mkn) && nrec > LONGREC); lb; lb &= lb - 1) {
+        const int w = __builtin_ctzll(lb);
+        const int nw = __builtin_amdgcn_readlane(nrec, w), bw = __builtin_amdgcn_readlane(base, w);
+        const bool cw = __builtin_amdgcn_readlane((int)cpy, w) != 0, mw = __builtin_amdgcn_readlane((int)mkn, w) != 0;
+        const int x0 = __builtin_amdgcn_readlane(xb0, w), x1 = __builtin_amdgcn_readlane(xb1, w);
+        const int x2 = __builtin_amdgcn_readlane(xb2, w), x3 = __builtin_amdgcn_readlane(xb3, w);
+        unsigned long long* const tw_ = ws.stmp + (size_t)(blockIdx.x * SPEC_BS + wb + w) * SPEC_RL;
+        for (int k = lane; k < nw; k += 64) {
+          const unsigned long long r = *spec_rec_at(tw_, ws.sxp, k, x0, x1, x2, x3);
+          if (cw) ws.slog[bw + k] = r;
+          if (mw) mark(r);
+        }
+      }
+      for (unsigned long long lb = __ballot(mkp && prv.y > LONGREC); lb; lb &= lb - 1) {
+        const int w = __builtin_ctzll(lb);
+        const int px = __builtin_amdgcn_readlane(prv.x, w), py_ = __builtin_amdgcn_readlane(prv.y, w);
+        for (int k = lane; k < py_; k += 64) mark(ws.slog[px + k]);
       }
     }
     fcand = wave_min(fcand);
@@ -1218,8 +1332,8 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
       // the round's longest wave with its wait / cascade split (10 ns ticks, 20 bits each)
       atomicMax(&ctl->spec.rmax, ((unsigned long long)tot << 40) | ((unsigned long long)min(tw, 0xfffffll) << 20) |
                                      (unsigned long long)min(tc, 0xfffffll));
-      // ... and its dealing + promotion / post-execution split (the same wave unless two tie)
-      atomicMax(&ctl->spec.rmax2, ((unsigned long long)tot << 40) | ((unsigned long long)min(tpr, 0xfffffll) << 20) |
+      // ... and its cooperative-cascade / post-execution split (the same wave unless two tie)
+      atomicMax(&ctl->spec.rmax2, ((unsigned long long)tot << 40) | ((unsigned long long)min(tco, 0xfffffll) << 20) |
                                       (unsigned long long)min(tpo, 0xfffffll));
     }
   }

@@ -42,6 +42,15 @@ def main():
                   d[1] / n, d[2] / n, 100.0 * d[2] / tot, d[3] / n, 100.0 * d[3] / tot, d[4] / n, 100.0 * d[4] / tot,
                   d[5], d[6] / max(1, d[5])),
               flush=True)
+        seg.set_diag(4)  # bank 3: the cooperative pops' phase split (cycles, summed)
+        seg.watershed_dev(ti, tm, tl)
+        torch.cuda.synchronize()
+        c = seg.stats()["diag"]
+        seg.set_diag(False)
+        nco = max(1, d[5])
+        print("%s: cooperative pop, cycles by phase: loads issued + hole %.0f, load wait %.0f, previous writes %.0f, "
+              "decide %.0f, pushes + record %.0f, select %.0f" % (nm, c[0] / nco, c[1] / nco, c[2] / nco, c[3] / nco,
+                                                                  c[4] / nco, c[5] / nco), flush=True)
         # wall-clock split of the round kernels (diag bank 1, 10 ns ticks): wave time in top-pop
         # waits / cascades / whole kernel, and the sum over rounds of each round's longest wave
         seg.set_diag(1)
@@ -57,7 +66,7 @@ def main():
         d = st["diag"]
         w = max(1, d[7])
         print("%s: flood %.1f ms (diag on) | waves %d, %.1f us each | sum of the rounds' longest waves %.1f ms over"
-              " %d rounds (%.1f us/round): dealing + promotion %.1f ms, top-pop waits %.1f ms, top-pop writes +"
+              " %d rounds (%.1f us/round): cooperative cascades %.1f ms, top-pop waits %.1f ms, top-pop writes +"
               " cascades %.1f ms, log copy + change marks %.1f ms" % (
                   nm, t0.elapsed_time(t1), d[7], d[2] / w / 100, d[5] / 1e5, st["spec_rounds"],
                   d[5] / 100 / max(1, st["spec_rounds"]), d[0] / 1e5, d[4] / 1e5, d[6] / 1e5, d[1] / 1e5), flush=True)
