@@ -89,6 +89,7 @@ typedef struct msg_stats {
     int64_t resolve_items;      /* items of the batches k_resolve decided (its re-runs included) */
     int64_t spec_exec_pops;     /* pops k_spec_round ran pop by pop: the top pops and cascade pops
                                    of every execution that was not replayed, over all rounds     */
+    int64_t spec_longest_pops;  /* sum over the rounds of each round's longest such execution    */
 } msg_stats;
 
 #define MSG_NKERNELS 24

@@ -613,6 +613,7 @@ int flood_end(msg_ctx* c, FloodRun& fr, int32_t* d_labels, int depth = 0, const 
   c->stats.scatter_pushes = tail.spushes;
   c->stats.resolve_items = tail.ritems;
   c->stats.spec_exec_pops = tail.spec.xpops;
+  c->stats.spec_longest_pops = tail.spec.xlong;
   // when speculative generations ran, diag reports their round split instead (spec_kernels.hip)
   for (int k = 0; k < 8; ++k)
 #ifdef MSEG_CF_PROF

@@ -187,6 +187,19 @@ __device__ __forceinline__ int spec_decide_own(const SpecView& V, const SpecRec&
   return c1 ? v1 : c2 ? v2 : c3 ? v3 : v4;
 }
 
+// the same for another item's view (the top pop's gather): final claims, the previous round's, state
+__device__ __forceinline__ int spec_decide_other(const SpecView& V, const SpecRec& r, int j) {
+  const unsigned long long f = r.fin;
+  const unsigned long long c = V.par ? r.cl0 : r.cl1;
+  const int lp = (int)(uint32_t)(V.par ? r.labs : (r.labs >> 32));
+  const bool c2 = (unsigned)(f >> 33) == V.G;
+  const bool c3 = V.hasprev & (sc_tag(c) == V.T - 1) & (sc_rank(c) < j);
+  const int v2 = ((f >> 32) & 1ull) ? (int)(uint32_t)f : INQ;
+  const int v3 = (c & 1ull) ? lp : INQ;
+  const int v4 = (r.s >= WSHED) ? r.s : INQ;
+  return c2 ? v2 : c3 ? v3 : v4;
+}
+
 // top-pop granule of item k as item j may use it in round T: this round's, or a final item's.
 // Word: label | round tag << 32 | (label differs from item k's previous round) << 63; chg
 // collects that bit of the non-final items read (an input of the reader changed).
@@ -249,6 +262,8 @@ __device__ void spec_finalize(Ctl* ctl, int P, int n, unsigned T, unsigned G, un
   const int ov = __hip_atomic_load(&ctl->sovf.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int newP = min(fc, n);
   s.rounds_total += 1;
+  s.xlong += __hip_atomic_load(&s.rxmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  s.rxmax = 0;
   s.ov2 = s.ov1;
   s.ov1 = ov;
   if (newP >= n) {
@@ -731,7 +746,7 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
             continue;
           }
         }
-        const int v = spec_decide(V, rr[d], j, false);
+        const int v = spec_decide_other(V, rr[d], j);
         if (v > 0) base_lab = fold_lab(base_lab, v);
         else if (v == 0) zm |= 1u << d;
       }
@@ -1099,16 +1114,16 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
         pf_q += nq + 1;
 #endif
         int v[4];
-        v[0] = spec_decide(V, r0, j, true);
-        v[1] = spec_decide(V, r1, j, true);
-        v[2] = spec_decide(V, r2, j, true);
-        v[3] = spec_decide(V, r3, j, true);
+        v[0] = spec_decide_own(V, r0, j);
+        v[1] = spec_decide_own(V, r1, j);
+        v[2] = spec_decide_own(V, r2, j);
+        v[3] = spec_decide_own(V, r3, j);
   #pragma unroll
-        for (int d = 0; d < 4; ++d) {  // the pending pop's writes, not in memory yet
-          if (nby[d] == py) v[d] = plab;
+        for (int d = 0; d < 4; ++d) {  // the pending pop's writes, not in memory yet (selects)
+          bool inq = false;
   #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (((ppm >> e) & 1u) && nby[d] == pz[e]) v[d] = INQ;
+          for (int e = 0; e < 4; ++e) inq |= (((ppm >> e) & 1u) != 0) & (nby[d] == pz[e]);
+          v[d] = inq ? INQ : (nby[d] == py) ? plab : v[d];
         }
         int lab = 0;
   #pragma unroll
@@ -1314,7 +1329,9 @@ __global__ __launch_bounds__(SPEC_BS, SPEC_MINB) void k_spec_round(Ws ws) {
     }
     fcand = wave_min(fcand);
     ocand = wave_min(ocand);
+    const int wxmax = -wave_min((ex && rbase < 0) ? -nrec : 0);  // the wave's longest execution
     if (lane == 0) {
+      if (wxmax > 0) atomicMax(&ctl->spec.rxmax, wxmax);
       // ranks are dealt in increasing order: once a lower rank is in, later waves skip the atomic
       if (fcand != NONE) atomicMin(&ctl->sfc.v, fcand);
       if (ocand != NONE) atomicMin(&ctl->sovf.v, ocand);
@@ -1500,19 +1517,20 @@ __global__ __launch_bounds__(SPEC_FT) void k_spec_flatten(Ws ws) {
       // the regime's start: slower per committed pop (small generations: a round costs launch
       // floors and its longest execution; frequent fallbacks) -> serial pops for a while
       const long long now = (long long)__builtin_amdgcn_s_memrealtime();
-      const long long el = now - s.tstart;
       s.gpops_total += Vn;
-      s.gticks_total += now - s.tgen;
+      s.gticks_total += now - s.tgen;  // (measured: reported in msg_stats, never judged on)
       ++s.accg;
-      const bool judge = s.accg >= SPEC_JUDGE_GENS || (s.accg >= 4 && el > SPEC_JUDGE_TICKS);
-      // judged on the generations' own time (+ a commit estimate each) per pop they committed,
-      // not on the wall time since the regime started: a fallback's serial pops cost the same
-      // either way (round 3 A/B: neutral on every frame, profiles/r03l_ab_regimes.log)
+      // judged on the generations' modelled time (ws_shared.h: rounds and each round's longest
+      // execution, + a commit estimate each) per pop they committed, not on the wall time since
+      // the regime started: a fallback's serial pops cost the same either way (round 3 A/B:
+      // neutral on every frame, profiles/r03l_ab_regimes.log)
       // (leaving the generations that fell back out of this judgement kept the regime on where it
       // re-ran the rest of a bucket after every long cascade: uniform noise at 4096^2 went from 15.7
       // to 48 s, round 4)
-      s.tspec += now - s.tgen + SPEC_COMMIT_TICKS;
+      s.tspec += (long long)SPEC_ROUND_TICKS * s.rounds + (long long)SPEC_POP_TICKS * (s.xlong - s.gxlong0) +
+                 SPEC_COMMIT_TICKS;
       s.pspec += Vn;
+      const bool judge = s.accg >= SPEC_JUDGE_GENS || (s.accg >= 4 && s.tspec > SPEC_JUDGE_TICKS);
       const bool slow = judge && s.tspec > (long long)SPEC_SERIAL_TICKS * s.pspec;
       if (s.fallback) {
         // the batch engine pops the overflowing item and its cascade (serial pops); the regime

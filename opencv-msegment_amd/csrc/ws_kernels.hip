@@ -835,6 +835,7 @@ __device__ void spec_begin(Ctl* ctl, Batch& nb, int L, int bstart, int navail) {
   s.fallback = 0;
   s.ftile = 0;
   s.tgen = (long long)__builtin_amdgcn_s_memrealtime();
+  s.gxlong0 = s.xlong;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -82,12 +82,21 @@ constexpr int SPEC_MAXREC_SHORT = 256;  // pops an execution may run (more: a ca
 constexpr int SPEC_ROUNDS_MAX = 64; // rounds per generation before the stable prefix is committed
 constexpr int SPEC_FT = 1024;       // items per k_spec_flatten tile
 constexpr int SPEC_QUIET = 4096;    // a generation this large without a cascade ends the regime
-constexpr int SPEC_SERIAL_TICKS = 100;       // ~1 us per serial pop (10 ns ticks): a regime
-constexpr int SPEC_JUDGE_GENS = 16;          // slower than that per committed pop (its fallbacks'
-                                             // serial pops included), after this many
-                                             // generations, ends for
+// The regime is judged on COUNTS, not on the clock (round 5): a generation is priced by a model of
+// its device time fitted to the round-5 flood probes -- 37 us per round (launches, gather, dealing,
+// the round's end) + 1.9 us per pop of each round's longest execution (a round lasts as long as
+// its longest cascade; spec_longest_pops) -- against serial pops at 0.8 us each.  The wall clock
+// it replaced flipped decisions whenever the device stalled (a first flood's allocations, a
+// profiler, concurrent floods): album.jpg's flood varied 1084-1497 ms from run to run.  A/B of the
+// serial price (profiles/r05k_regime_probe*.log): 0.5 us -> album.jpg 1226 ms (mostly serial pops,
+// 0.53 us each there), 0.8 us -> 1088 ms; notConnectedMarkers' seeds at 1024^2 882 / 921 ms.
+constexpr int SPEC_ROUND_TICKS = 3700;       // model: 10 ns ticks per round
+constexpr int SPEC_POP_TICKS = 190;          // model: ticks per pop of a round's longest execution
+constexpr int SPEC_SERIAL_TICKS = 80;        // ~0.8 us per serial pop: a regime slower than that per
+constexpr int SPEC_JUDGE_GENS = 16;          // committed pop (its fallbacks' serial pops included),
+                                             // after this many generations, ends for
 constexpr int SPEC_COOL_POPS = 65536;        // this many serial pops (doubling per repeat)
-constexpr int SPEC_JUDGE_TICKS = 200000;     // slow generations are judged after 4 once 2 ms passed
+constexpr int SPEC_JUDGE_TICKS = 200000;     // slow generations are judged after 4 once 2 ms (model) passed
 constexpr int SPEC_COMMIT_TICKS = 3000;      // ~30 us: a generation's ordered append (k_scan, k_scatter)
 
 // A tiled pixel's speculative-generation words (k_spec_round reads a neighbour's whole record
@@ -121,8 +130,9 @@ struct SpecCtl {
   long long tstart, pstart;  // regime start: s_memrealtime, Ctl.pops
   long long tgen;            // s_memrealtime at the current generation's start (spec_begin)
   long long gpops_total, gticks_total;  // whole flood: pops the generations committed, their time
-  long long tspec, pspec;    // since the regime start: generations' own time (+ a commit estimate
-                             // each) and the pops they committed -- what the regime is judged on
+  long long tspec, pspec;    // since the regime start: generations' modelled time (+ a commit
+                             // estimate each) and the pops they committed -- what the regime is
+                             // judged on
   long long gens, rounds_total, execs, cpops, fallbacks;
   unsigned long long rmax;  // diagnostics: longest wave of this round (10 ns ticks) | waits | cascades
   unsigned long long rmax2; // ... | its dealing + promotion | its post-execution work
@@ -132,6 +142,11 @@ struct SpecCtl {
   long long replays;        // executions whose cascade was replayed from the previous round
   long long xpops;          // pops k_spec_round ran pop by pop (top pops + cascade pops of the
                             // executions that were not replayed): its algorithmic unit
+  int rxmax;                // this round's longest execution run pop by pop (pops)
+  int pad_x;
+  long long xlong;          // sum over the flood's rounds of rxmax (a round lasts about as long as
+                            // its longest execution)
+  long long gxlong0;        // xlong at the current generation's start
 };
 
 // desc word of a batch item: bits 0-31 the 4 edge weights, 32-35 push (or 0-neighbour) mask,

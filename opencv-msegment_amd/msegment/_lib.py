@@ -67,7 +67,8 @@ class Stats(ctypes.Structure):
                 ("spec_gen_us", ctypes.c_int64),
                 ("fast_pops", ctypes.c_int64), ("fast_pushes", ctypes.c_int64),
                 ("scatter_pops", ctypes.c_int64), ("scatter_pushes", ctypes.c_int64),
-                ("resolve_items", ctypes.c_int64), ("spec_exec_pops", ctypes.c_int64)]
+                ("resolve_items", ctypes.c_int64), ("spec_exec_pops", ctypes.c_int64),
+                ("spec_longest_pops", ctypes.c_int64)]
 
 
 class KernelProfile(ctypes.Structure):

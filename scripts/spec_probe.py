@@ -59,10 +59,11 @@ def main():
         st = seg.stats()
         px = m.size
         line = ("%-22s %9.1f ms %8.2f Mpx/s | pops %d batches %d | gens %d rounds %d execs/pop %.2f cpops %d "
-                "fallbacks %d cools %d replays %d gen_pops %d gen_ms %.1f" % (
+                "fallbacks %d cools %d replays %d gen_pops %d gen_ms %.1f xpops %d longest %d" % (
                     nm, ms, px / ms / 1e3, st["pops"], st["batches"], st["spec_generations"], st["spec_rounds"],
                     st["spec_executions"] / max(1, st["pops"]), st["spec_cascade_pops"], st["spec_fallbacks"],
-                    st["spec_cooldowns"], st["spec_replays"], st["spec_gen_pops"], st["spec_gen_us"] / 1e3))
+                    st["spec_cooldowns"], st["spec_replays"], st["spec_gen_pops"], st["spec_gen_us"] / 1e3,
+                    st["spec_exec_pops"], st["spec_longest_pops"]))
         ok = ""
         if do_oracle:
             from oracle import ws_oracle
