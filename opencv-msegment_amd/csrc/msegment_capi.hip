@@ -84,7 +84,7 @@ struct msg_ctx {
   bool prof = false;
   unsigned long long* d_diag = nullptr;  // 8 counters when diagnostics are on
   bool diag = false;
-  int diag_bank = 0;  // msg_set_diag(ctx, 3 / 4): report bank 2 (the small-batch loop's regime split) / 3
+  int diag_bank = 0;  // msg_set_diag(ctx, 3): report bank 2 (the small-batch loop's regime split)
   int inject = 0;  // msg_set_diag(ctx, 2): k_resolve give-up injection (tests)
   std::vector<hipEvent_t> evpool;
   size_t evused = 0;
@@ -619,7 +619,7 @@ int flood_end(msg_ctx* c, FloodRun& fr, int32_t* d_labels, int depth = 0, const 
 #ifdef MSEG_CF_PROF
     c->stats.diag[k] = (int64_t)dgv[8 + k];  // k_commit_fast's phase split (diagnostic build)
 #else
-    c->stats.diag[k] = (int64_t)dgv[c->diag_bank >= 2 ? 8 * c->diag_bank + k : tail.spec.gens ? 8 + k : k];
+    c->stats.diag[k] = (int64_t)dgv[c->diag_bank == 2 ? 16 + k : tail.spec.gens ? 8 + k : k];
 #endif
   c->stats.spec_generations = tail.spec.gens;
   c->stats.spec_rounds = tail.spec.rounds_total;
@@ -1190,7 +1190,7 @@ int msg_set_diag(msg_ctx* c, int enable) {
   }
   c->diag = enable != 0;
   c->inject = enable == 2;
-  c->diag_bank = enable == 3 ? 2 : enable == 4 ? 3 : 0;
+  c->diag_bank = enable == 3 ? 2 : 0;
   return MSG_OK;
 }
 

@@ -501,18 +501,6 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
 #ifdef MSEG_SPEC_PROF
   const long long c_t0 = (long long)__builtin_amdgcn_s_memtime();
   const int c_n0 = S.nrec;
-  // bank 3 (msg_set_diag 4): cycles of a cooperative pop by phase -- loads issued + hole fixed,
-  // the wait for the loads, the previous pop's writes, decide, pushes + record, select
-  long long c_ph[6] = {0, 0, 0, 0, 0, 0};
-  long long c_tq = 0;
-  auto c_mark = [&](int k) {
-    const long long t = (long long)__builtin_amdgcn_s_memtime();
-    c_ph[k] += t - c_tq;
-    c_tq = t;
-  };
-#define COOP_MARK(k) c_mark(k)
-#else
-#define COOP_MARK(k) (void)0
 #endif
   for (;;) {
     // ---- the length caps and the record chunk of pop nrec, as at the per-lane loop's head ----
@@ -533,9 +521,6 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
       else S.xb3 = b;
     }
     // ---- the pop of y: its loads (lanes 0-3 one neighbour each), then the previous pop's writes ----
-#ifdef MSEG_SPEC_PROF
-    c_tq = (long long)__builtin_amdgcn_s_memtime();
-#endif
     const int yb = y + marg;
     int nb[4];  // uniform: scalar arithmetic, then one lane per direction
 #pragma unroll
@@ -564,11 +549,8 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
       }
       fix = -1;
     }
-    COOP_MARK(0);
     vm_drain();
-    COOP_MARK(1);
     if (S.pwrite) coop_writes();
-    COOP_MARK(2);
     // ---- decide: lanes 0-3, patched with the previous pop's writes (issued after these loads) ----
     int v = 0;
     {
@@ -590,7 +572,6 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
       S.ovf = true;
       lab = WSHED;
     }
-    COOP_MARK(3);
     unsigned dmy = 0, pmy = 0;
     if (lab != WSHED) {
 #pragma unroll
@@ -613,7 +594,6 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
     S.pz3 = nb[3];
     S.pwrite = true;
     ++S.nrec;
-    COOP_MARK(4);
     if (S.ovf || H + S.nc == 0) break;
     // ---- select: the smallest ord of all columns ----
     if (H == 0) {
@@ -624,7 +604,6 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
     fix = __builtin_ctzll(__ballot(m1 == m));
     y = __builtin_amdgcn_readlane(m1pix, fix);
     --H;
-    COOP_MARK(5);
     // the loop-carried state is wave-uniform: say so, so that the loop's branches stay scalar
     H = __builtin_amdgcn_readfirstlane(H);
     rr = __builtin_amdgcn_readfirstlane(rr);
@@ -638,13 +617,10 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
   }
   if (S.pwrite) coop_writes();  // the last pop's
 #ifdef MSEG_SPEC_PROF
-  if (ws.diag && lane == 0) {  // bank 2: cooperative pops, their cycles; bank 3: the phase split
+  if (ws.diag && lane == 0) {  // bank 2: cooperative pops, their cycles
     atomicAdd(&ws.diag[21], (unsigned long long)(S.nrec - c_n0));
     atomicAdd(&ws.diag[22], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - c_t0));
-#pragma unroll
-    for (int k = 0; k < 6; ++k) atomicAdd(&ws.diag[24 + k], (unsigned long long)c_ph[k]);
   }
-#undef COOP_MARK
 #endif
 }
 

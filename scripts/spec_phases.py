@@ -42,15 +42,6 @@ def main():
                   d[1] / n, d[2] / n, 100.0 * d[2] / tot, d[3] / n, 100.0 * d[3] / tot, d[4] / n, 100.0 * d[4] / tot,
                   d[5], d[6] / max(1, d[5])),
               flush=True)
-        seg.set_diag(4)  # bank 3: the cooperative pops' phase split (cycles, summed)
-        seg.watershed_dev(ti, tm, tl)
-        torch.cuda.synchronize()
-        c = seg.stats()["diag"]
-        seg.set_diag(False)
-        nco = max(1, d[5])
-        print("%s: cooperative pop, cycles by phase: loads issued + hole %.0f, load wait %.0f, previous writes %.0f, "
-              "decide %.0f, pushes + record %.0f, select %.0f" % (nm, c[0] / nco, c[1] / nco, c[2] / nco, c[3] / nco,
-                                                                  c[4] / nco, c[5] / nco), flush=True)
         # wall-clock split of the round kernels (diag bank 1, 10 ns ticks): wave time in top-pop
         # waits / cascades / whole kernel, and the sum over rounds of each round's longest wave
         seg.set_diag(1)
