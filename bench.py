@@ -892,6 +892,7 @@ def main(argv=None):
                       "pushes": st["pushes"], "host_syncs": st["host_syncs"]},
             "kernels": kern,
             "parity": parity,
+            "build_id": msegment._lib.load().msg_build_id().decode(),
         }
         print(json.dumps(out), flush=True)
     seg.close()
