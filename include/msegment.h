@@ -100,6 +100,11 @@ typedef struct msg_kernel_profile {
 } msg_kernel_profile;
 
 /* One context per thread: owns a HIP stream and the device workspace on `device_ordinal`.
+ * Workspace, kept between calls and grown to the largest frame seen: ~44 B per pixel for the
+ * flood, plus ~88 B per tiled pixel and ~200 MB for the speculative-generation engine
+ * (DESIGN.md section 3a): allocated up front for frames of 2^20 tiled pixels or more when memory
+ * allows (otherwise on the first flood that enters the interrupt-dense regime), and on that first
+ * entry below that size.
  * flags: 0, or MSG_CREATE_HIGH_PRIORITY for a high-priority stream (the batch entry points'
  * internal sub-contexts use it: the HIP runtime keeps streams of different priorities on
  * different hardware queues, so concurrent floods overlap even at GPU_MAX_HW_QUEUES=4).

@@ -469,8 +469,15 @@ int flood_begin(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int H,
   fr.spec_bound = false;
   if (fr.spec && (c->spec_np > 0 || fr.ntiled >= (1ll << 20))) {  // (re)size and arm it now
     rc = ensure_spec(c, fr.ntiled, N, st);
-    if (rc) return rc;
-    fr.spec_bound = true;
+    if (rc == MSG_ENOMEM) {  // out of memory up front: the lazy path (only a flood that enters
+      free_spec(c);          // the regime needs the engine, and it fails there if memory is short)
+      (void)hipGetLastError();
+      c->err.clear();
+    } else if (rc) {
+      return rc;
+    } else {
+      fr.spec_bound = true;
+    }
   }
   bind_spec(c, fr, fr.spec_bound);
   const int npx = (int)((N + CH - 1) / CH);

@@ -177,9 +177,9 @@ __device__ __forceinline__ int spec_decide_own(const SpecView& V, const SpecRec&
   const unsigned long long f = r.fin;
   const unsigned long long c = V.par ? r.cl0 : r.cl1;
   const int lp = (int)(uint32_t)(V.par ? r.labs : (r.labs >> 32));
-  const bool c1 = (sc_tag(o) == V.T) & (sc_rank(o) == j);  // (no short-circuit: no branches)
+  const bool c1 = (int)(sc_tag(o) == V.T) & (int)(sc_rank(o) == j);  // (no short-circuit: no branches)
   const bool c2 = (unsigned)(f >> 33) == V.G;
-  const bool c3 = V.hasprev & (sc_tag(c) == V.T - 1) & (sc_rank(c) < j);
+  const bool c3 = (int)V.hasprev & (int)(sc_tag(c) == V.T - 1) & (int)(sc_rank(c) < j);
   const int v1 = (o & 1ull) ? lc : INQ;
   const int v2 = ((f >> 32) & 1ull) ? (int)(uint32_t)f : INQ;
   const int v3 = (c & 1ull) ? lp : INQ;
@@ -193,7 +193,7 @@ __device__ __forceinline__ int spec_decide_other(const SpecView& V, const SpecRe
   const unsigned long long c = V.par ? r.cl0 : r.cl1;
   const int lp = (int)(uint32_t)(V.par ? r.labs : (r.labs >> 32));
   const bool c2 = (unsigned)(f >> 33) == V.G;
-  const bool c3 = V.hasprev & (sc_tag(c) == V.T - 1) & (sc_rank(c) < j);
+  const bool c3 = (int)V.hasprev & (int)(sc_tag(c) == V.T - 1) & (int)(sc_rank(c) < j);
   const int v2 = ((f >> 32) & 1ull) ? (int)(uint32_t)f : INQ;
   const int v3 = (c & 1ull) ? lp : INQ;
   const int v4 = (r.s >= WSHED) ? r.s : INQ;

@@ -1211,6 +1211,7 @@ __global__ __launch_bounds__(RBS, 4) void k_resolve(Ws ws) {
   // process a completed chunk out of step with the block (re-runs under concurrent floods)
   __shared__ int s_skip[2], s_yield;
   __shared__ unsigned long long s_ctag;  // this run's chunk claims: {epoch, re-run}
+  __shared__ unsigned long long s_tl[RBS];  // the chunk's granules, for dependencies inside the block
   if (tid == 0) s_ctag = etag | (unsigned)B.rrun;
   if (work && blockIdx.x == 0 && tid == 0) {
     ctl->rsv = B.epoch;  // k_scan commits only decided batches
@@ -1227,11 +1228,26 @@ __global__ __launch_bounds__(RBS, 4) void k_resolve(Ws ws) {
       if (!sk) __hip_atomic_store(&ws.cflag[2 * chunk], s_ctag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tid < NQ) hist[tid] = 0;
+    s_tl[tid] = 0;
     __syncthreads();
     if (s_skip[par]) continue;
     const int wbase = base + (tid & ~63);
     const int i = wbase + lane;
     const bool valid = i < B.n;
+    // a dependency on another wave of the block reads its granule from LDS (every wave of the
+    // block is resident, so such a wait cannot outlast its writer); the global granule serves the
+    // other blocks.  Measured: k_resolve 23.85 -> 23.37 us at 4096^2, the headline flat
+    // (profiles/r05o_ab_resolve.log; merging the push phase's granule loads into the label
+    // phase's round trip, or 1024-thread blocks, measured slower)
+    auto gld = [&](int r) -> unsigned long long {
+      return ((unsigned)(r - base) < (unsigned)RBS)
+                 ? __hip_atomic_load(&s_tl[r - base], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                 : ld_granule(&ws.tl[r]);
+    };
+    auto gst = [&](unsigned long long v) {
+      __hip_atomic_store(&s_tl[tid], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      st_granule(&ws.tl[i], v);
+    };
     const unsigned long long t_a = dg ? __builtin_amdgcn_s_memtime() : 0;
     Item it;
     int sg = 0;
@@ -1297,7 +1313,7 @@ __global__ __launch_bounds__(RBS, 4) void k_resolve(Ws ws) {
             v = snap[d];
             pb = sbase[d];
           } else {
-            const unsigned long long g = ld_granule(&ws.tl[r]);
+            const unsigned long long g = gld(r);
             const unsigned long long hi = g & 0xffffffff00000000ull;
             v = (hi == etag) ? (int)(uint32_t)g : 0;
             pb = (hi == ptag) ? (int)(uint32_t)g : 0;
@@ -1314,7 +1330,7 @@ __global__ __launch_bounds__(RBS, 4) void k_resolve(Ws ws) {
           if (((pm >> d) & 1u) && prov[d] != WSHED && !(prov[d] > 0 && prov[d] == lab)) unknown = true;
         if (unknown && lab != WSHED) {
           if (!published && it.base_lab != 0) {  // let later items see this one's base fold
-            st_granule(&ws.tl[i], ptag | (uint32_t)it.base_lab);
+            gst(ptag | (uint32_t)it.base_lab);
             published = true;
           }
         } else {
@@ -1323,7 +1339,7 @@ __global__ __launch_bounds__(RBS, 4) void k_resolve(Ws ws) {
             lab = WSHED;
           }
           mylab = lab;
-          st_granule(&ws.tl[i], etag | (uint32_t)lab);
+          gst(etag | (uint32_t)lab);
           lab_done = true;
         }
       }
@@ -1356,7 +1372,7 @@ __global__ __launch_bounds__(RBS, 4) void k_resolve(Ws ws) {
               if ((unsigned)(r - wbase) < 64u) {
                 v = psnap[3 * d + k];
               } else {
-                const unsigned long long g = ld_granule(&ws.tl[r]);
+                const unsigned long long g = gld(r);
                 v = ((g & 0xffffffff00000000ull) == etag) ? (int)(uint32_t)g : 0;
               }
               if (v > 0) lose = true;

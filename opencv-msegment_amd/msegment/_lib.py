@@ -120,9 +120,9 @@ def load():
     except ImportError:
         pass
     L = ctypes.CDLL(LIB_PATH)
+    L.msg_build_id.argtypes = []
+    L.msg_build_id.restype = ctypes.c_char_p
     if not os.environ.get("MSEGMENT_LIB") and os.path.isdir(CSRC):
-        L.msg_build_id.argtypes = []
-        L.msg_build_id.restype = ctypes.c_char_p
         # the in-tree library must be built from the sources next to it: a stale .so (shipped to a
         # box that did not rebuild) would silently run old kernels.  MSEGMENT_LIB (A/B builds of
         # other variants) is taken as given.
