@@ -1,6 +1,6 @@
 """The headline step (4096^2 mosaic, device-resident watershed + colorise) against the k_resolve
 grid size (msg_set_resolve_grid; 0 = the default, one wave of the device's occupancy), interleaved
-passes.  usage: python scripts/resolve_grid_probe.py"""
+passes.  usage: python scripts/resolve_grid_probe.py [grid ...]  (default 0 640 512 384 256)"""
 import os
 import sys
 import time
@@ -22,8 +22,9 @@ def main():
     ti, tm = torch.from_numpy(img).to(dev), torch.from_numpy(m).to(dev)
     tl = torch.empty_like(tm)
     dst = torch.empty((S, S, 3), dtype=torch.uint8, device=dev)
+    grids = [int(a) for a in sys.argv[1:]] or [0, 640, 512, 384, 256]
     for rep in range(2):
-        for g in (0, 640, 512, 384, 256):
+        for g in grids:
             seg.set_resolve_grid(g)
             for _ in range(3):
                 seg.watershed_colorize_dev(ti, tm, tl, depth, None, dst)
@@ -33,7 +34,9 @@ def main():
                 seg.watershed_colorize_dev(ti, tm, tl, depth, None, dst)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / 20
-            print("rep %d grid %4s: %.3f ms  %.0f Mpx/s" % (rep, g or "dflt", dt * 1e3, S * S / dt / 1e6), flush=True)
+            st = seg.stats()
+            print("rep %d grid %4s: %.3f ms  %.0f Mpx/s  resolve items %d" % (rep, g or "dflt", dt * 1e3, S * S / dt / 1e6,
+                                                                            st["resolve_items"]), flush=True)
     seg.close()
 
 
