@@ -34,7 +34,7 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
 done
 # the library these counters (and the bench line) come from, for the PMC files' notes
 BID=$(python -c "import sys; sys.path.insert(0, 'opencv-msegment_amd'); from msegment import _lib; print(_lib.load().msg_build_id().decode())")
-python scripts/pmc_summary.py "$OUT" "$OUT/pmc_latest.json" "$TAG, libmsegment build $BID; single-flood command" > "$OUT/pmc_summary.log" 2>&1
+python scripts/pmc_summary.py "$OUT" "$OUT/pmc_latest.json" "$TAG, libmsegment build $BID; single-flood command" $PROF_ARGS > "$OUT/pmc_summary.log" 2>&1
 # the config-3 stress variants (speculative engine, serial pops): kernel stats and HBM traffic
 if [ -n "${STRESS_PROF:-}" ]; then
   for kind in mosaic_noise random; do
@@ -45,7 +45,7 @@ if [ -n "${STRESS_PROF:-}" ]; then
       run pmc_${kind}_$ctr 900 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_$kind/pmc_$ctr" -o run -- python bench.py $SARGS
     done
     python scripts/pmc_summary.py "$OUT/pmc_$kind" "$OUT/pmc_stress_$kind.json" \
-      "$TAG, libmsegment build $BID: config-3 stress variant $kind as the main step" --kind $kind > "$OUT/pmc_summary_$kind.log" 2>&1
+      "$TAG, libmsegment build $BID: config-3 stress variant $kind as the main step" $SARGS > "$OUT/pmc_summary_$kind.log" 2>&1
   done
 fi
 echo "== done"

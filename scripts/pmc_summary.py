@@ -58,8 +58,8 @@ def main():
                   "fetch_bytes_per_launch": 2.0 * 1024.0 * fk / max(fn, 1),
                   "write_bytes_per_launch": 1024.0 * wk / max(wn, 1)}
         res[k]["hbm_bytes_per_launch"] = res[k]["fetch_bytes_per_launch"] + res[k]["write_bytes_per_launch"]
-    doc = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs) of "
-                     "`python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass --batch-frames 1`",
+    cmd = " ".join(sys.argv[4:]) or "--steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass --batch-frames 1"
+    doc = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs) of `python bench.py %s`" % cmd,
            "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes", "note": sys.argv[3] if len(sys.argv) > 3 else "",
            "config": bench_config(sys.argv[4:]), "kernels": res}
     json.dump(doc, open(out, "w"), indent=1)
