@@ -131,7 +131,10 @@ int  msg_get_kernel_profile(msg_ctx* ctx, msg_kernel_profile* out, int max_entri
  * first chunk of every batch once, which exercises the give-up / re-run path.
  * enable == 3 reports the regime split instead: tiny batches, their pops, their time
  * (s_memrealtime, 10 ns ticks); serial pops, their time; two reserved counters; pops of small
- * batches (65..4096 items). */
+ * batches (65..4096 items).
+ * enable == 4 (the -DMSEG_SPEC_PROF diagnostic build) reports the wave-cooperative cascade
+ * pop's phases instead (s_memtime cycles summed over pops): loads issued + queue fix, the wait
+ * for the loads, writes + decision, pushes, select; counters 5..7 are 0. */
 int  msg_set_diag(msg_ctx* ctx, int enable);
 /* Speculative generations for the interrupt-dense regime (textured frames, scattered seeds):
  * on by default.  enable = 0 keeps the batch engine's serial pops there instead (A/B runs and

@@ -626,7 +626,7 @@ int flood_end(msg_ctx* c, FloodRun& fr, int32_t* d_labels, int depth = 0, const 
 #ifdef MSEG_CF_PROF
     c->stats.diag[k] = (int64_t)dgv[8 + k];  // k_commit_fast's phase split (diagnostic build)
 #else
-    c->stats.diag[k] = (int64_t)dgv[c->diag_bank == 2 ? 16 + k : tail.spec.gens ? 8 + k : k];
+    c->stats.diag[k] = (int64_t)dgv[c->diag_bank == 2 ? 16 + k : c->diag_bank == 3 ? 24 + k : tail.spec.gens ? 8 + k : k];
 #endif
   c->stats.spec_generations = tail.spec.gens;
   c->stats.spec_rounds = tail.spec.rounds_total;
@@ -1099,7 +1099,7 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
       msg_destroy(c);
       return MSG_EHIP;
     }
-    // one full wave of k_resolve blocks (3 x 512 threads per CU at its 80 VGPRs, capped at 4):
+    // one full wave of k_resolve blocks (2 x 512 threads per CU at its 96 VGPRs, capped at 4):
     // a performance choice only -- chunks are dealt in dispatch order, so progress does not
     // depend on how many of the blocks are resident (msg_set_resolve_grid overrides it)
     c->res_grid = cus * std::max(1, std::min(per, 4));
@@ -1197,7 +1197,7 @@ int msg_set_diag(msg_ctx* c, int enable) {
   }
   c->diag = enable != 0;
   c->inject = enable == 2;
-  c->diag_bank = enable == 3 ? 2 : 0;
+  c->diag_bank = enable == 3 ? 2 : enable == 4 ? 3 : 0;
   return MSG_OK;
 }
 

@@ -502,6 +502,12 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
   const long long c_t0 = (long long)__builtin_amdgcn_s_memtime();
   const int c_n0 = S.nrec;
 #endif
+#ifdef MSEG_SPEC_PROF
+  long long cp0 = 0, cp1 = 0, cp2 = 0, cp3 = 0, cp4 = 0, cta = 0, ctb = 0;
+#define CP_T(v) v = (long long)__builtin_amdgcn_s_memtime()
+#else
+#define CP_T(v) do { } while (0)
+#endif
   for (;;) {
     // ---- the length caps and the record chunk of pop nrec, as at the per-lane loop's head ----
     if (S.nrec >= (longok ? SPEC_MAXREC : SPEC_MAXREC_SHORT)) {
@@ -520,6 +526,7 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
       else if (c == 2) S.xb2 = b;
       else S.xb3 = b;
     }
+    CP_T(cta);
     // ---- the pop of y: its loads (lanes 0-3 one neighbour each), then the previous pop's writes ----
     const int yb = y + marg;
     int nb[4];  // uniform: scalar arithmetic, then one lane per direction
@@ -549,7 +556,15 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
       }
       fix = -1;
     }
+#ifdef MSEG_SPEC_PROF
+    CP_T(ctb);
+    cp0 += ctb - cta;
+#endif
     vm_drain();
+#ifdef MSEG_SPEC_PROF
+    CP_T(cta);
+    cp1 += cta - ctb;
+#endif
     if (S.pwrite) coop_writes();
     // ---- decide: lanes 0-3, patched with the previous pop's writes (issued after these loads) ----
     int v = 0;
@@ -572,6 +587,10 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
       S.ovf = true;
       lab = WSHED;
     }
+#ifdef MSEG_SPEC_PROF
+    CP_T(ctb);
+    cp2 += ctb - cta;
+#endif
     unsigned dmy = 0, pmy = 0;
     if (lab != WSHED) {
 #pragma unroll
@@ -583,6 +602,10 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
         else dmy |= 1u << d;
       }
     }
+#ifdef MSEG_SPEC_PROF
+    CP_T(cta);
+    cp3 += cta - ctb;
+#endif
     S.prec = srec_pack(y, lab, dmy);
     S.sig = smix(S.sig, S.prec);
     S.py = y;
@@ -614,7 +637,21 @@ __device__ __forceinline__ void spec_coop(const Ws& ws, const SpecView& V, unsig
     S.qseq = (unsigned)__builtin_amdgcn_readfirstlane((int)S.qseq);
     S.ovf = __builtin_amdgcn_readfirstlane((int)S.ovf) != 0;
     S.cap = __builtin_amdgcn_readfirstlane((int)S.cap) != 0;
+#ifdef MSEG_SPEC_PROF
+    CP_T(ctb);
+    cp4 += ctb - cta;
+#endif
   }
+#undef CP_T
+#ifdef MSEG_SPEC_PROF
+  if (ws.diag && lane == 0) {  // bank 3: the cooperative pop's phases (cycles)
+    atomicAdd(&ws.diag[24], (unsigned long long)cp0);
+    atomicAdd(&ws.diag[25], (unsigned long long)cp1);
+    atomicAdd(&ws.diag[26], (unsigned long long)cp2);
+    atomicAdd(&ws.diag[27], (unsigned long long)cp3);
+    atomicAdd(&ws.diag[28], (unsigned long long)cp4);
+  }
+#endif
   if (S.pwrite) coop_writes();  // the last pop's
 #ifdef MSEG_SPEC_PROF
   if (ws.diag && lane == 0) {  // bank 2: cooperative pops, their cycles

@@ -121,8 +121,9 @@ class Segmenter:
 
     def set_diag(self, on=True):
         """In-kernel counters; on=2 also injects k_resolve give-ups (tests of the re-run path);
-        on=3 reports the one-workgroup loop's regime split instead (msegment.h, msg_set_diag)."""
-        self._check(self._L.msg_set_diag(self._h, int(on) if on in (2, 3) else (1 if on else 0)))
+        on=3 reports the one-workgroup loop's regime split instead, on=4 the cooperative cascade
+        pop's phases (diagnostic build; msegment.h, msg_set_diag)."""
+        self._check(self._L.msg_set_diag(self._h, int(on) if on in (2, 3, 4) else (1 if on else 0)))
 
     def set_fast_commit(self, on=True):
         """Two-launch iterations for large flood batches (default on); off = three launches."""

@@ -1,7 +1,7 @@
 """Config 5 per GPU (8 mosaic 4096^2 frames per call) against the k_resolve grid size and the number
 of floods in flight: does a smaller per-flood grid let concurrent floods share the chip?
 (Round 4 also swept the commit grid's share through an environment knob, since removed.)
-usage: python scripts/batch_grid_probe.py"""
+usage: python scripts/batch_grid_probe.py [grids (0 = default) [floods in flight]], e.g. "0,384,256" "4,8"."""
 import os
 import sys
 import time
@@ -25,8 +25,10 @@ def main():
     labs = [torch.empty_like(m) for m in mks]
     dsts = [torch.empty((S, S, 3), dtype=torch.uint8, device=dev) for _ in frames]
     depth = max(f[2] for f in frames)
-    for grid in (0, 384, 256, 128):
-        for inflight in (4, 8):
+    grids = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 384, 256, 128]
+    flights = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [4, 8]
+    for grid in grids:
+        for inflight in flights:
             seg.set_resolve_grid(grid)
             seg.set_batch_inflight(inflight)
             seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)

@@ -42,6 +42,18 @@ def main():
                   d[1] / n, d[2] / n, 100.0 * d[2] / tot, d[3] / n, 100.0 * d[3] / tot, d[4] / n, 100.0 * d[4] / tot,
                   d[5], d[6] / max(1, d[5])),
               flush=True)
+        # the wave-cooperative pop's phases (diag bank 3, s_memtime cycles summed over pops)
+        seg.set_diag(4)
+        seg.watershed_dev(ti, tm, tl)
+        torch.cuda.synchronize()
+        st3 = seg.stats()
+        seg.set_diag(False)
+        c = st3["diag"]
+        tot3 = max(1, sum(c[:5]))
+        print("%s: cooperative pop phases (cycles per pop over %d pops): loads issued + queue fix %.0f, wait for"
+              " the loads %.0f, writes + decision %.0f, pushes %.0f, select %.0f (%.0f%% waiting)" % (
+                  nm, d[5], c[0] / max(1, d[5]), c[1] / max(1, d[5]), c[2] / max(1, d[5]), c[3] / max(1, d[5]),
+                  c[4] / max(1, d[5]), 100.0 * c[1] / tot3), flush=True)
         # wall-clock split of the round kernels (diag bank 1, 10 ns ticks): wave time in top-pop
         # waits / cascades / whole kernel, and the sum over rounds of each round's longest wave
         seg.set_diag(1)
