@@ -1099,7 +1099,7 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
       msg_destroy(c);
       return MSG_EHIP;
     }
-    // one full wave of k_resolve blocks (2 x 512 threads per CU at its 96 VGPRs, capped at 4):
+    // one full wave of k_resolve blocks (3 x 512 threads per CU at its 80 VGPRs, capped at 4):
     // a performance choice only -- chunks are dealt in dispatch order, so progress does not
     // depend on how many of the blocks are resident (msg_set_resolve_grid overrides it)
     c->res_grid = cus * std::max(1, std::min(per, 4));

@@ -1186,8 +1186,13 @@ __device__ __attribute__((noinline)) bool orphan_below(const unsigned long long*
   return orphan;
 }
 
+// 6 waves per SIMD: 80 VGPRs (32 B of scratch per lane for spills), so three
+// 512-thread blocks per CU and a block-round of 768 x 512 items: the batches of 262 145-393 216
+// items, which at the 96-VGPR build's two blocks per CU took a second block-round of the whole
+// round-trip chain, take one (k_resolve 22.7 -> 21.6 us, headline 5088 -> 5180 Mpx/s, batch
+// 9204 -> 9366; 8 waves: 64 VGPRs, 4970: profiles/r05zy_ab_resolve_waves.log)
 template <bool INJECT>
-__global__ __launch_bounds__(RBS, 4) void k_resolve(Ws ws) {
+__global__ __launch_bounds__(RBS) __attribute__((amdgpu_waves_per_eu(6))) void k_resolve(Ws ws) {
   Ctl* ctl = ws.ctl;
   __shared__ Seg segs[NQ];
   __shared__ int hist[NQ];

@@ -17,7 +17,7 @@ constexpr int INQ = -2;          // cv::watershed IN_QUEUE, before the pixel has
 __host__ __device__ inline int queued_state(int slot) { return -3 - slot; }
 __host__ __device__ inline int state_slot(int state) { return -3 - state; }
 constexpr int NONE = 0x7fffffff;
-constexpr int RBS = 512;           // threads per k_resolve block (2 per CU at its 128-VGPR budget)
+constexpr int RBS = 512;           // threads per k_resolve block (3 per CU at its 80-VGPR budget)
 constexpr int SMALL_MAX = 4096;    // batches up to this size run in k_scan's one-workgroup loop
 constexpr int PAL_LDS_MAX = 16384; // palettes up to this many labels are staged in LDS
 constexpr int MERGE_CAP = 1 << 22; // largest multi-segment batch (items)
