@@ -1186,11 +1186,12 @@ __device__ __attribute__((noinline)) bool orphan_below(const unsigned long long*
   return orphan;
 }
 
-// 6 waves per SIMD: 80 VGPRs (32 B of scratch per lane for spills), so three
-// 512-thread blocks per CU and a block-round of 768 x 512 items: the batches of 262 145-393 216
-// items, which at the 96-VGPR build's two blocks per CU took a second block-round of the whole
-// round-trip chain, take one (k_resolve 22.7 -> 21.6 us, headline 5088 -> 5180 Mpx/s, batch
-// 9204 -> 9366; 8 waves: 64 VGPRs, 4970: profiles/r05zy_ab_resolve_waves.log)
+// 6 waves per SIMD: 80 VGPRs, so three 512-thread blocks per CU and a block-round of 768 x 512
+// items: the batches of 262 145-393 216 items, which at the 96-VGPR build's two blocks per CU took
+// a second block-round of the whole round-trip chain, take one (k_resolve 22.7 -> 21.6 us,
+// headline 5088 -> 5180 Mpx/s, batch 9204 -> 9366; 8 waves: 64 VGPRs, 4970:
+// profiles/r05zy_ab_resolve_waves.log).  Without scratch (see the chunk loop's end): 5283, batch
+// 9620 (profiles/r05zz_ab_resolve_nospill.log)
 template <bool INJECT>
 __global__ __launch_bounds__(RBS) __attribute__((amdgpu_waves_per_eu(6))) void k_resolve(Ws ws) {
   Ctl* ctl = ws.ctl;
@@ -1471,8 +1472,14 @@ __global__ __launch_bounds__(RBS) __attribute__((amdgpu_waves_per_eu(6))) void k
       }
       break;
     }
-    if (tid < NQ && hist[tid]) atomicAdd(&ws.cnt[(long long)(base / CH) * NQ + tid], hist[tid]);
-    if (tid == 0) __hip_atomic_store(&ws.cflag[2 * chunk + 1], B.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the row address and the epoch are formed here: hoisted out of the chunk loop they were two
+    // 64-bit values live across the whole kernel, which the 80-VGPR budget spilled to scratch
+    // (16 B written per thread per launch)
+    int t = tid;
+    unsigned ep = B.epoch;
+    asm volatile("" : "+v"(t), "+s"(ep));
+    if (t < NQ && hist[t]) atomicAdd(&ws.cnt[(long long)(base / CH) * NQ + t], hist[t]);
+    if (t == 0) __hip_atomic_store(&ws.cflag[2 * chunk + 1], (unsigned long long)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   }
   __syncthreads();
