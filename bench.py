@@ -12,9 +12,12 @@ through libmsegment's device entry point msg_watershed_colorize_dev.
   python bench.py --pipeline color                      # colorAutoMarkerWatershed's
       marker stage (sharpen, Otsu, chamfer distance, contours) + the flood of the sharpened frame
 
-N > 1 (launched by torch.distributed.run, one rank per GPU): every rank segments its own frame
-(BASELINE config 5: batched frames, one per GPU, no collectives -- weak scaling).  The only
-collectives are the timing barriers and the max-over-ranks of the elapsed time.
+N > 1 (launched by torch.distributed.run, one rank per GPU): BASELINE config 5 -- rank r floods
+config 5's frames 100 + 8r .. 100 + 8r + 7 as ONE batch call per step, 4 floods in flight (weak
+scaling: 8 frames per GPU; at N = 8 the 64 frames of config 5).  Every rank checks its 8 label maps
+against the committed oracle digests and the counts are summed over ranks ("64/64 frames bit-exact"
+at N = 8).  The data path has no collectives; the only ones are the timing barriers, the
+max-over-ranks of the elapsed time and that parity sum.
 
 Rank 0 prints ONE JSON line.  Extra objects: "roofline" (dominant kernel, HIP-event timed on the
 launch stream), "cpu_baseline" (the C oracle = same algorithm, timed on this host, rank 0, N=1),
@@ -74,12 +77,44 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")  # scripts/pmc_s
 E2E_BYTES_PER_PIXEL = 14.0                  # 3 B BGR + 4 B markers in, 4 B labels + 3 B BGR out
 
 
-def frame_seed(seed, rank, world):
-    """The frame a rank segments: --seed, else config 3's seed 2 on one GPU, else config 5's frame
-    100 + rank (frames 100 + k; replicas, one frame stream per GPU, no collectives)."""
+def frame_seed(seed, rank, world, frames=1):
+    """The first frame a rank segments: --seed, else config 3's seed 2 on one GPU, else config 5's
+    frame 100 + frames * rank (config 5's frames are 100 + k, k = 0..63; with 8 frames
+    per rank, rank r takes 100 + 8r .. 100 + 8r + 7; replicas, no collectives)."""
     if seed is not None:
         return seed
-    return 2 if world == 1 else 100 + rank
+    return 2 if world == 1 else 100 + frames * rank
+
+
+def default_frames(frames, world):
+    """Frames per rank per step: --frames, else 1 on one GPU (the headline config 3 step) and
+    BASELINE config 5's 8 per GPU (64 frames over 8 GPUs) when N > 1."""
+    if frames is not None:
+        return max(1, frames)
+    return 1 if world == 1 else 8
+
+
+def digest_parity(labels, keys, dgs):
+    """(checked, bad): label maps (numpy int32) against the committed oracle digests of `keys`;
+    frames without a digest are not counted."""
+    checked = bad = 0
+    for lab, key in zip(labels, keys):
+        if key in dgs:
+            checked += 1
+            bad += hashlib.sha256(lab.tobytes()).hexdigest() != dgs[key]["labels_sha256"]
+    return checked, bad
+
+
+def reduce_sum_ints(vals, device=None):
+    """Element-wise sum of a small int list over the ranks (identity on one rank)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return list(vals)
+    t = torch.tensor(list(vals), dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [int(v) for v in t.tolist()]
 
 
 def log(*a):
@@ -538,20 +573,42 @@ def stress_line(seg, S, sync, dev, steps, cpu=True, kind="mosaic_noise", seed=2)
     return out
 
 
+def pmc_build_id(pm):
+    """The libmsegment build a PMC summary's counters came from (its "build_id", or the id its note
+    names: scripts/gpu_check.sh writes "libmsegment build <id>")."""
+    import re
+
+    if pm.get("build_id"):
+        return pm["build_id"]
+    m = re.search(r"build ([0-9a-f]{16})", pm.get("note", ""))
+    return m.group(1) if m else None
+
+
 def pmc_traffic(kernel, cfg):
     """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/pmc_*.json,
-    scripts/pmc_summary.py), only from a file collected on this same workload `cfg`."""
+    scripts/pmc_summary.py), only from a file collected on this same workload `cfg` AND on the
+    library build this process loaded: counters of another build are not quoted (traffic None, the
+    source says which build they came from)."""
     import glob
 
+    import msegment
+
+    here = msegment._lib.load().msg_build_id().decode()
+    stale = None
     for path in [PMC_SUMMARY] + sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
         if not os.path.exists(path):
             continue
         pm = json.load(open(path))
         kk = pm.get("kernels", {}).get(kernel)
         if kk and pm.get("config") == cfg:
+            bid = pmc_build_id(pm)
+            if bid != here:
+                stale = stale or "not quoted: %s holds counters of build %s, this library is build %s" % (
+                    os.path.relpath(path, ROOT), bid, here)
+                continue
             return round(kk["hbm_bytes_per_launch"]), "%s (%s; %s)" % (
                 os.path.relpath(path, ROOT), pm.get("correction"), pm.get("note", ""))
-    return None, None
+    return None, stale
 
 
 def colour_distance(seg, t_img, img, S, sync, pmc_cfg, reps=20, check=True):
@@ -642,10 +699,10 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=None, help="default 3 (nc: 1)")
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--kind", default="mosaic", choices=["mosaic", "mosaic_noise", "random"])
-    ap.add_argument("--seed", type=int, default=None, help="default: 2 (N=1), 100+rank (N>1)")
-    ap.add_argument("--frames", type=int, default=1,
-                    help="frames per rank per step (BASELINE config 5: 64 frames over 8 GPUs = 8); "
-                         "default 1 = the headline single-frame step")
+    ap.add_argument("--seed", type=int, default=None, help="default: 2 (N=1), 100+frames*rank (N>1)")
+    ap.add_argument("--frames", type=int, default=None,
+                    help="frames per rank per step; default 1 on one GPU (the headline single-frame "
+                         "step, config 3) and 8 when N > 1 (BASELINE config 5: 64 frames over 8 GPUs)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="floods kept in flight together when --frames > 1")
     ap.add_argument("--batch-frames", type=int, default=8,
@@ -688,18 +745,29 @@ def main(argv=None):
     import msegment
     from msegment import synth
 
+    # MSEG_BENCH_SHARED_GPU=1 (rehearsal of the N > 1 path on a one-GPU box): every rank on GPU 0
+    # and gloo for the timing / parity collectives (RCCL refuses two ranks on one GPU); the line says
+    # so.  Never set by the driver's runs.
+    shared = bool(os.environ.get("MSEG_BENCH_SHARED_GPU")) and world > 1
+    if shared:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    cdev = None if shared else dev  # where the collectives' tensors live
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if shared:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     barrier = (lambda: dist.barrier()) if world > 1 else (lambda: None)
     sync = torch.cuda.synchronize
 
     S = args.size
-    seed = frame_seed(args.seed, rank, world)
+    K = default_frames(args.frames, world)
+    seed = frame_seed(args.seed, rank, world, K)
     # the workload the PMC passes must have been collected on for their traffic to be quoted
-    pmc_cfg = {"pipeline": args.pipeline, "kind": args.kind, "size": S, "seed": seed, "frames": max(1, args.frames)}
+    pmc_cfg = {"pipeline": args.pipeline, "kind": args.kind, "size": S, "seed": seed, "frames": K}
     t0 = time.perf_counter()
     img, m, depth = synth.frame(args.kind, S, S, seed)
     log("[rank %d] generated %s %dx%d seed %d in %.1fs" % (rank, args.kind, S, S, seed, time.perf_counter() - t0))
@@ -708,7 +776,6 @@ def main(argv=None):
     t_lab = torch.empty_like(t_m)
     t_dst = torch.empty((S, S, 3), dtype=torch.uint8, device=dev)
     seg = msegment.Segmenter(local)
-    K = max(1, args.frames)
     if K > 1:  # K frames (seeds seed..seed+K-1) per step, up to --inflight floods in flight
         extra = [synth.frame(args.kind, S, S, seed + k) for k in range(1, K)]
         b_img = [t_img] + [torch.from_numpy(f[0]).to(dev) for f in extra]
@@ -774,14 +841,24 @@ def main(argv=None):
     parity = None
     dgs = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
     dkey = "%s_%dx%d_s%d" % (args.kind, S, S, seed)
-    if rank == 0 and dkey in dgs and not MARKERS:  # committed oracle digest of this frame
-        got = hashlib.sha256(t_lab.cpu().numpy().tobytes()).hexdigest()
-        parity = ("bit-exact vs oracle digest" if got == dgs[dkey]["labels_sha256"]
-                  else "MISMATCH vs oracle digest") + " " + dkey
-        log("[rank 0] parity:", parity)
+    if not MARKERS:
+        # every rank: each of its K label maps against its committed oracle digest, summed over ranks
+        keys = ["%s_%dx%d_s%d" % (args.kind, S, S, seed + k) for k in range(K)]
+        labs_now = [t_lab.cpu().numpy()] if K == 1 else [x.cpu().numpy() for x in b_lab]
+        checked, bad = reduce_sum_ints(digest_parity(labs_now, keys, dgs), cdev)
+        del labs_now
+        if K == 1 and world == 1:
+            if checked:
+                parity = ("bit-exact vs oracle digest" if not bad else "MISMATCH vs oracle digest") + " " + dkey
+        elif checked:
+            parity = "%d/%d frames bit-exact vs oracle digests (%s frames %d..%d over %d rank%s)" % (
+                checked - bad, checked, args.kind, frame_seed(args.seed, 0, world, K),
+                frame_seed(args.seed, world - 1, world, K) + K - 1, world, "s" if world > 1 else "")
+        if rank == 0:
+            log("[rank 0] parity:", parity)
 
     dt = timed_steps(step, args.steps, barrier, sync)
-    dt_max = reduce_max(dt, dev)
+    dt_max = reduce_max(dt, cdev)
     value = whole_job_mpx(world, K * S * S, args.steps, dt_max)
     ms_per_step = 1000.0 * dt_max / args.steps
     log("[rank %d] %.3f ms/step (max over ranks %.3f)" % (rank, 1000 * dt / args.steps, ms_per_step))
@@ -868,7 +945,8 @@ def main(argv=None):
             "data": "synthetic (msegment.synth %s, splitmix64; regenerated on the box)" % args.kind,
             "config": {"workload": "%s %dx%d seed %s%s, %s + colorByIndexes(colored=false), "
                                    "device-resident (BASELINE config %s)"
-                                   % (args.kind, S, S, seed if (world == 1 or args.seed is not None) else "100+rank",
+                                   % (args.kind, S, S, seed if (world == 1 or args.seed is not None)
+                                      else "100+%d*rank" % K,
                                       "" if K == 1 else "..+%d, %d floods in flight" % (K - 1, min(K, args.inflight)),
                                       ("notConnectedMarkers marker stage (depth %d, %s; %d levels) + watershed"
                                        % (args.nc_depth, "+".join(nc_opts) or "no options", len(nc_levels)))
@@ -880,7 +958,9 @@ def main(argv=None):
                                       ({1024: "2", 4096: "3", 16384: "4 frame on one GPU"}.get(
                                           S, "-: a %d-pixel frame" % (S * S)) if K == 1
                                        else "5 batching") if world == 1 else "5"),
-                       "frames_per_rank_per_step": K, "parallelism": "replicas%d (no collectives)" % world},
+                       "frames_per_rank_per_step": K, "parallelism": "replicas%d (no collectives)" % world,
+                       **({"rehearsal": "MSEG_BENCH_SHARED_GPU: all %d ranks on GPU 0, gloo collectives "
+                                        "(not a multi-GPU measurement)" % world} if shared else {})},
             "roofline": roof,
             "colour_distance": stencil,
             "batch": batch,

@@ -48,7 +48,7 @@ extern "C" {
 #define MSG_ERANGE   (-6)  /* output array too small / search space beyond what the
                               reference could finish (documented per entry point)          */
 
-#define MSG_ABI_VERSION 6
+#define MSG_ABI_VERSION 7
 
 typedef struct msg_ctx msg_ctx;
 
@@ -66,7 +66,8 @@ typedef struct msg_stats {
                                rounds of the round's longest wave's wave-cooperative cascades
                                and of its log copy + change marks; wave time in the round kernel;
                                longest wave; sums over the rounds of the longest wave's top-pop
-                               waits, of its whole time, of its top-pop writes + cascades; waves */
+                               waits, of its whole time, of its top-pop writes + cascades; waves.
+                               Single floods only: 0 after a batch call (the frames' banks differ) */
     /* speculative generations (the interrupt-dense regime; msg_set_speculative) */
     int64_t spec_generations;   /* generations committed                                        */
     int64_t spec_rounds;        /* rounds run (every generation needs >= 2: run + confirm)      */
@@ -184,6 +185,22 @@ int msg_watershed_colorize_batch(msg_ctx* ctx, int n, const uint8_t* const* bgr,
 
 /* Floods kept in flight by the batch entry points (1..8, default 4; 1 = back to back). */
 int msg_set_batch_inflight(msg_ctx* ctx, int k);
+
+/* Host-buffer batches over several devices (BASELINE config 5: 64 frames, one frame stream per GPU,
+ * no collectives).  After this call msg_watershed_batch and msg_watershed_colorize_batch split
+ * their n frames into ndev contiguous blocks -- block j = frames [n*j/ndev, n*(j+1)/ndev) -- and run
+ * block j on an internal sub-context on devices[j] (one host thread per entry; each sub-context
+ * keeps this context's msg_set_batch_inflight / msg_set_batch_floods / speculative / fast-commit
+ * settings).  With 8 entries 0..7 and 64 frames, device r floods frames 8r..8r+7 -- the frames
+ * bench.py's rank r takes.  A device may repeat (e.g. {0, 0}: two sub-contexts on one GPU).
+ * ndev = 0 restores this context's own device.  Device-pointer batches (the _dev entry) are not
+ * affected: their buffers live on one device.  Each entry costs a context and its workspace
+ * (~44 B/px of the largest frame it flooded) on its device, released by ndev = 0 or msg_destroy.
+ * The reference's JVM reaches it through MSegmentNative.watershedBatch(..., devices) (INTEGRATION.md
+ * section 5); it replaces a loop of PictureService.watershed calls (PictureService.java:908) that
+ * can only use the JVM's one context device.  MSG_EINVAL for ndev < 0 or > 64, a null list, or a
+ * device ordinal outside [0, hipGetDeviceCount()). */
+int msg_set_batch_devices(msg_ctx* ctx, int ndev, const int* devices);
 
 /* Many floods per launch in the batch entry points (msg_watershed_batch,
  * msg_watershed_colorize_batch, msg_watershed_colorize_batch_dev), for frames whose exact flood is serial-bound -- photographs,

@@ -104,6 +104,13 @@ struct msg_ctx {
   int wss_cap = 0;
   uint8_t* d_mstage = nullptr;   // host-buffer many-floods batches: every frame's image + markers
   long long mstage_cap = 0;
+  // host-buffer batches over several devices (msg_set_batch_devices): the device list and one
+  // sub-context per entry (created on first use), each running its contiguous block of frames
+  std::vector<int> bdevs;
+  std::vector<msg_ctx*> dsubs;
+  // the eager speculative workspace failed with ENOMEM for frames of this many tiled pixels: frames
+  // at least this large go straight to the lazy path (cleared by msg_set_speculative)
+  long long spec_eager_failed_np = 0;
   // marker stage: device histogram + its pinned host mirror, gray scratch
   int cus = 0;
   unsigned* d_hist = nullptr;  // 256 bins
@@ -467,12 +474,15 @@ int flood_begin(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int H,
   fr.ntiled = (long long)((H + 3) / 4) * ws.Wt * 16;
   fr.spec = c->spec && !multi && fr.ntiled <= (1ll << 28) && H >= 3 && W >= 3;
   fr.spec_bound = false;
-  if (fr.spec && (c->spec_np > 0 || fr.ntiled >= (1ll << 20))) {  // (re)size and arm it now
+  const bool eager_failed = c->spec_eager_failed_np > 0 && fr.ntiled >= c->spec_eager_failed_np;
+  if (fr.spec && (c->spec_np >= fr.ntiled || (!eager_failed && (c->spec_np > 0 || fr.ntiled >= (1ll << 20))))) {
     rc = ensure_spec(c, fr.ntiled, N, st);
     if (rc == MSG_ENOMEM) {  // out of memory up front: the lazy path (only a flood that enters
       free_spec(c);          // the regime needs the engine, and it fails there if memory is short)
       (void)hipGetLastError();
       c->err.clear();
+      // remembered: later floods of this size or larger skip the failing eager allocation
+      c->spec_eager_failed_np = fr.ntiled;
     } else if (rc) {
       return rc;
     } else {
@@ -695,8 +705,10 @@ int upload_palette(msg_ctx* c, const uint8_t* pal, int depth, hipStream_t st) {
 
 constexpr int MAX_INFLIGHT = 8;
 
-// Batch totals: every counter of msg_stats summed over the frames (diag included), the frame size
-// of the last one.
+// Batch totals: every counter of msg_stats summed over the frames, the frame size of the last one.
+// diag is zeroed: a frame's diag is one of several banks (k_resolve cycles with a max-type slot, or
+// the speculative round split), chosen per frame, so sums over frames would mix units and add
+// maxima (msegment.h: diag is reported for single floods only).
 void add_stats(msg_stats& tot, const msg_stats& s) {
   static_assert(sizeof(msg_stats) % sizeof(int64_t) == 0, "msg_stats is int64 fields only");
   int64_t* t = reinterpret_cast<int64_t*>(&tot);
@@ -704,6 +716,7 @@ void add_stats(msg_stats& tot, const msg_stats& s) {
   for (size_t k = 0; k < sizeof(msg_stats) / sizeof(int64_t); ++k) t[k] += a[k];
   tot.rows = s.rows;
   tot.cols = s.cols;
+  for (auto& d : tot.diag) d = 0;
 }
 
 int ensure_subs(msg_ctx* c, int k) {
@@ -1129,6 +1142,9 @@ void msg_destroy(msg_ctx* c) {
   c->subs.clear();
   for (msg_ctx* sub : c->msubs) msg_destroy(sub);
   c->msubs.clear();
+  for (msg_ctx* sub : c->dsubs) msg_destroy(sub);  // other devices: each switches the thread's device
+  c->dsubs.clear();
+  (void)hipSetDevice(c->dev);
   dfree(c->d_wss);
   dfree(c->d_mstage);
   free_stage(c);
@@ -1175,11 +1191,14 @@ int msg_set_fast_commit(msg_ctx* c, int enable) {
 int msg_set_speculative(msg_ctx* c, int enable) {
   if (!c) return MSG_EINVAL;
   c->spec = enable != 0;
+  c->spec_eager_failed_np = 0;
   if (!c->spec) free_spec(c);  // the engine's workspace comes back on its next first use
   for (msg_ctx* sub : c->subs) {
     sub->spec = c->spec;
     if (!sub->spec) free_spec(sub);
   }
+  for (msg_ctx* sub : c->dsubs)
+    if (sub) (void)msg_set_speculative(sub, enable);
   return MSG_OK;
 }
 
@@ -1411,6 +1430,75 @@ int msg_colorize(msg_ctx* c, const int32_t* labels, size_t label_stride, int row
 
 namespace {
 
+int host_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size_t* bgr_stride, int32_t* const* markers,
+               const size_t* marker_stride, const int* rows, const int* cols, int depth, const uint8_t* palette,
+               uint8_t* const* dst, const size_t* dst_stride);
+
+// msg_set_batch_devices: frames [n*j/D, n*(j+1)/D) on the sub-context of device-list entry j, one
+// host thread per entry, each a host_batch of its own (this context's batch settings copied over).
+// No data crosses devices: every block's buffers are the caller's host memory.
+int spread_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size_t* bgr_stride, int32_t* const* markers,
+                 const size_t* marker_stride, const int* rows, const int* cols, int depth, const uint8_t* palette,
+                 uint8_t* const* dst, const size_t* dst_stride) {
+  const int D = (int)c->bdevs.size();
+  c->dsubs.resize(D, nullptr);
+  for (int j = 0; j < D; ++j) {
+    msg_ctx*& x = c->dsubs[j];
+    if (!x) {
+      const int rc = msg_create(&x, c->bdevs[j], 0);
+      if (rc) {
+        x = nullptr;
+        return fail(c, rc, "sub-context on device %d (entry %d) failed (%d)", c->bdevs[j], j, rc);
+      }
+    }
+    x->inflight = c->inflight;
+    x->fast = c->fast;
+    if (c->res_grid_set) {
+      x->res_grid = c->res_grid;
+      x->res_grid_set = true;
+    }
+    if (x->spec != c->spec) {
+      const int rc = msg_set_speculative(x, c->spec ? 1 : 0);
+      if (rc) return fail(c, rc, "%s", x->err.c_str());
+    }
+    if (x->many != c->many) {
+      const int rc = msg_set_batch_floods(x, c->many);
+      if (rc) return fail(c, rc, "%s", x->err.c_str());
+    }
+    if (x->diag != c->diag || x->inject != c->inject) {
+      const int rc = msg_set_diag(x, c->inject ? 2 : c->diag ? 1 : 0);
+      if (rc) return fail(c, rc, "%s", x->err.c_str());
+    }
+  }
+  std::vector<int> rcs(D, MSG_OK);
+  std::vector<std::thread> th;
+  for (int j = 0; j < D; ++j)
+    th.emplace_back([&, j]() {
+      msg_ctx* x = c->dsubs[j];
+      const int lo = (int)((long long)n * j / D), hi = (int)((long long)n * (j + 1) / D);
+      x->stats = msg_stats{};
+      if (hi == lo) return;
+      if (hipSetDevice(x->dev) != hipSuccess) {
+        rcs[j] = fail(x, MSG_EHIP, "hipSetDevice(%d) failed", x->dev);
+        return;
+      }
+      rcs[j] = host_batch(x, hi - lo, bgr + lo, bgr_stride + lo, markers + lo, marker_stride + lo, rows + lo,
+                          cols + lo, depth, palette, dst ? dst + lo : nullptr, dst ? dst_stride + lo : nullptr);
+    });
+  for (auto& t : th) t.join();
+  msg_stats tot{};
+  for (int j = 0; j < D; ++j) {
+    if (rcs[j]) {
+      c->err = "device " + std::to_string(c->dsubs[j]->dev) + " (entry " + std::to_string(j) +
+               "): " + c->dsubs[j]->err;
+      return rcs[j];
+    }
+    if ((long long)n * (j + 1) / D > (long long)n * j / D) add_stats(tot, c->dsubs[j]->stats);
+  }
+  c->stats = tot;
+  return MSG_OK;
+}
+
 // The host-buffer batch (msg_watershed_batch, msg_watershed_colorize_batch): labels in place, and
 // the colourised frames when dst is given.  Many-floods mode: every frame staged (image, markers,
 // colour output, each 16-B aligned), flooded together, read back; otherwise run_batch.
@@ -1428,6 +1516,8 @@ int host_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size_t* bgr_s
     if (dst && (long long)rows[k] * cols[k] > 0 && (!dst[k] || dst_stride[k] < (size_t)cols[k] * 3))
       return fail(c, MSG_EINVAL, "dst of frame %d: null or stride too small", k);
   }
+  if (!c->bdevs.empty() && n > 0)
+    return spread_batch(c, n, bgr, bgr_stride, markers, marker_stride, rows, cols, depth, palette, dst, dst_stride);
   if (!(c->many && n > 0))
     return run_batch(c, n, [&](int k, msg_ctx* x) {
       return dst ? msg_watershed_colorize(x, bgr[k], bgr_stride[k], markers[k], marker_stride[k], rows[k], cols[k],
@@ -1566,8 +1656,36 @@ int msg_watershed_colorize_batch_dev(msg_ctx* c, int n, const void* const* d_bgr
   });
 }
 
+int msg_set_batch_devices(msg_ctx* c, int ndev, const int* devices) {
+  if (!c) return MSG_EINVAL;
+  if (ndev < 0 || ndev > 64 || (ndev > 0 && !devices))
+    return fail(c, MSG_EINVAL, "device list: %d entries%s (0..64)", ndev, ndev > 0 && !devices ? ", null" : "");
+  int count = 0;
+  if (ndev > 0 && (hipGetDeviceCount(&count) != hipSuccess || count <= 0))
+    return fail(c, MSG_EHIP, "hipGetDeviceCount failed");
+  for (int j = 0; j < ndev; ++j)
+    if (devices[j] < 0 || devices[j] >= count)
+      return fail(c, MSG_EINVAL, "device list entry %d: ordinal %d outside [0, %d)", j, devices[j], count);
+  // sub-contexts whose entry changed device (or was dropped) go; the others keep their workspaces
+  for (size_t j = 0; j < c->dsubs.size(); ++j)
+    if (c->dsubs[j] && ((int)j >= ndev || c->dsubs[j]->dev != devices[j])) {
+      msg_destroy(c->dsubs[j]);
+      c->dsubs[j] = nullptr;
+    }
+  c->dsubs.resize(ndev, nullptr);
+  c->bdevs.assign(devices, devices + ndev);
+  (void)hipSetDevice(c->dev);  // msg_destroy of a sub-context switched the thread's device
+  return MSG_OK;
+}
+
 int msg_set_batch_floods(msg_ctx* c, int mode) {
   if (!c || mode < 0 || mode > 2) return MSG_EINVAL;
+  for (msg_ctx* sub : c->dsubs)
+    if (sub) {
+      const int rc = msg_set_batch_floods(sub, mode);
+      if (rc) return fail(c, rc, "%s", sub->err.c_str());
+    }
+  (void)hipSetDevice(c->dev);
   c->many = mode;
   if (mode == 0) {  // the mode's per-frame workspaces (~44 B/px each) are released with it
     if (hipSetDevice(c->dev) != hipSuccess) return fail(c, MSG_EHIP, "hipSetDevice failed");

@@ -78,6 +78,11 @@ __device__ __forceinline__ void claim_max(unsigned long long* p, unsigned long l
 // of a loaded value is vmcnt(0) behind the writes too -- their acknowledgements (atomics at the L2
 // or beyond) then sat on every pop's critical path.  Issued after the wait, the writes complete
 // while the pop is decided and the next pop's loads are in flight.
+// The immediate is the gfx9 encoding (vmcnt[3:0] = 0, expcnt and lgkmcnt at their maxima, vmcnt[5:4]
+// = 0); gfx10+ lay the fields out differently, so any other target is refused at compile time.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "vm_drain: s_waitcnt 0x0F70 is vmcnt(0) only in the gfx9 encoding (build for gfx950)"
+#endif
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 __device__ __forceinline__ unsigned long long fin_word(unsigned G, unsigned popped, int lab) {

@@ -94,6 +94,22 @@ JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNativ
   return c ? msg_set_batch_floods(c, mode) : MSG_EINVAL;
 }
 
+// msg_set_batch_devices (msegment.h): the batch calls' frames split over a GPU list, block j on
+// devices[j] (config 5: one frame stream per GPU); an empty array = the context's own device.
+JNIEXPORT jint JNICALL Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_setBatchDevices(
+    JNIEnv* env, jclass, jlong ctx, jintArray devices) {
+  msg_ctx* c = reinterpret_cast<msg_ctx*>(ctx);
+  if (!c || !devices) return MSG_EINVAL;
+  const jsize n = env->GetArrayLength(devices);
+  if (n > 64) return MSG_EINVAL;
+  jint d[64];
+  env->GetIntArrayRegion(devices, 0, n, d);
+  if (env->ExceptionCheck()) return MSG_EINVAL;
+  int v[64];
+  for (jsize k = 0; k < n; ++k) v[k] = d[k];
+  return msg_set_batch_devices(c, n, n ? v : nullptr);
+}
+
 // PictureService.watershed over a batch of frames in one call (the reference's evaluation loop:
 // CorrelationTestService.java:84-86, 116, 128, 141 -> PictureService.java:852, 92 floods per
 // image): bgrs[k] (byte[]), markers[k] (int[], rewritten in place), dsts[k] (byte[]) of

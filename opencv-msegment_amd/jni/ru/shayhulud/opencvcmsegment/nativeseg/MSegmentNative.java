@@ -16,7 +16,10 @@ public final class MSegmentNative {
         System.loadLibrary("msegment_jni");   // links libmsegment.so
     }
 
-    private static final ThreadLocal<Long> CTX = ThreadLocal.withInitial(() -> create(0));
+    /** The GPU new thread contexts open on: -Dmsegment.device=N, or useDevice(N); 0 by default. */
+    private static volatile int defaultDevice = Integer.getInteger("msegment.device", 0);
+
+    private static final ThreadLocal<Long> CTX = ThreadLocal.withInitial(() -> open(defaultDevice));
 
     private MSegmentNative() {
     }
@@ -24,6 +27,33 @@ public final class MSegmentNative {
     private static native long create(int device);
 
     private static native void destroy(long ctx);
+
+    private static long open(int device) {
+        long ctx = create(device);
+        if (ctx == 0) {
+            throw new CvException("libmsegment: no context on device " + device);
+        }
+        return ctx;
+    }
+
+    /**
+     * Moves the calling thread's context to GPU {@code device} (its old context and workspace are
+     * released) and makes it the device later threads start on.  Replaces the fixed device 0.
+     */
+    public static void useDevice(int device) {
+        long fresh = open(device);
+        long old = CTX.get();
+        CTX.set(fresh);
+        BATCH_MODE.get()[0] = 0;
+        BATCH_DEVICES.set(new int[0]);
+        defaultDevice = device;
+        destroy(old);
+    }
+
+    /** msg_set_batch_devices: the host batches' device list (empty = the context's own device). */
+    private static native int setBatchDevices(long ctx, int[] devices);
+
+    private static final ThreadLocal<int[]> BATCH_DEVICES = ThreadLocal.withInitial(() -> new int[0]);
 
     /** Returns 0 or a negative MSG_E* code; markers rewritten in place, dst filled. */
     private static native int watershedColorize(long ctx, byte[] bgr, int[] markers, int rows, int cols,
@@ -174,7 +204,22 @@ public final class MSegmentNative {
      */
     public static java.util.List<Mat> watershedBatch(java.util.List<Mat> srcs, java.util.List<Mat> markers,
                                                      int depth, byte[] paletteOrNull, boolean manyFloods) {
+        return watershedBatch(srcs, markers, depth, paletteOrNull, manyFloods, new int[0]);
+    }
+
+    /**
+     * watershedBatch over several GPUs (BASELINE config 5: one frame stream per GPU, no collectives):
+     * the frames are split into devices.length contiguous blocks, block j flooded on GPU devices[j]
+     * (msg_set_batch_devices); an empty array keeps the thread's own device.  E.g. 64 frames on
+     * {0..7}: GPU r floods frames 8r..8r+7.
+     */
+    public static java.util.List<Mat> watershedBatch(java.util.List<Mat> srcs, java.util.List<Mat> markers,
+                                                     int depth, byte[] paletteOrNull, boolean manyFloods,
+                                                     int[] devices) {
         int n = srcs.size();
+        if (devices == null) {
+            throw new CvException("watershedBatch: null device list");
+        }
         if (markers.size() != n) {
             throw new CvException("watershedBatch: " + n + " images but " + markers.size() + " marker maps");
         }
@@ -207,6 +252,13 @@ public final class MSegmentNative {
                 throw new CvException("libmsegment error " + rc + ": " + lastError(ctx));
             }
             cur[0] = mode;
+        }
+        if (!java.util.Arrays.equals(BATCH_DEVICES.get(), devices)) {
+            int rc = setBatchDevices(ctx, devices);
+            if (rc != 0) {
+                throw new CvException("libmsegment error " + rc + ": " + lastError(ctx));
+            }
+            BATCH_DEVICES.set(devices.clone());
         }
         int rc = watershedColorizeBatch(ctx, bgr, lab, rows, cols, depth, paletteOrNull, out);
         if (rc != 0) {

@@ -200,8 +200,10 @@ class Segmenter:
         cols = (ctypes.c_int * n)()
         for k, (bgr, m) in enumerate(frames):
             bgr, st = _img_view(bgr)
-            if m.dtype != np.int32 or not m.flags.c_contiguous:
-                raise MsegError(_lib.MSG_EINVAL, "batch markers must be C-contiguous int32")
+            if not isinstance(m, np.ndarray) or m.dtype != np.int32 or m.ndim != 2 or not m.flags.c_contiguous:
+                raise MsegError(_lib.MSG_EINVAL, "batch markers must be C-contiguous int32 (H, W)")
+            if bgr.shape[:2] != m.shape:  # rows and cols come from the markers alone
+                raise MsegError(_lib.MSG_EINVAL, "frame %d: src and markers sizes differ" % k)
             keep.append(bgr)
             bp[k] = bgr.ctypes.data
             bs[k] = st
@@ -211,12 +213,15 @@ class Segmenter:
         if depth is None:
             self._check(self._L.msg_watershed_batch(self._h, n, bp, bs, mp, ms, rows, cols))
             return None
+        depth = int(depth)
+        pal = None
+        if palette is not None:  # the library reads 3 * depth bytes from it
+            pal = np.ascontiguousarray(palette, dtype=np.uint8).reshape(-1, 3)
+            if pal.shape[0] < depth:
+                raise MsegError(_lib.MSG_EINVAL, "palette has fewer than depth colours")
         dsts = [np.empty(m.shape + (3,), np.uint8) for _, m in frames]
         dp = (ctypes.c_void_p * n)(*[d.ctypes.data for d in dsts])
         ds = (ctypes.c_size_t * n)(*[d.shape[1] * 3 for d in dsts])
-        pal = None
-        if palette is not None:
-            pal = np.ascontiguousarray(palette, dtype=np.uint8)
         self._check(self._L.msg_watershed_colorize_batch(self._h, n, bp, bs, mp, ms, rows, cols, int(depth),
                                                           pal.ctypes.data if pal is not None else None, dp, ds))
         return dsts
@@ -224,6 +229,13 @@ class Segmenter:
     def set_batch_inflight(self, k):
         """Floods kept in flight by the batch calls (1..8; 1 = back to back)."""
         self._check(self._L.msg_set_batch_inflight(self._h, int(k)))
+
+    def set_batch_devices(self, devices=()):
+        """Spread the host-buffer batch calls over a device list (msg_set_batch_devices): frames
+        [n*j/D, n*(j+1)/D) run on devices[j]; () = this context's own device."""
+        devs = [int(d) for d in devices]
+        arr = (ctypes.c_int * max(1, len(devs)))(*devs)
+        self._check(self._L.msg_set_batch_devices(self._h, len(devs), arr if devs else None))
 
     def set_batch_floods(self, mode=1):
         """Many floods per launch in the batch calls (msegment.h msg_set_batch_floods): 0 off, 1 every

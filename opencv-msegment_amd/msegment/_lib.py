@@ -39,7 +39,7 @@ EXPORTS = (
     "msg_watershed_dev", "msg_colorize_dev", "msg_watershed_colorize_dev", "msg_edge_weights_dev",
     "msg_set_profiling", "msg_get_kernel_profile", "msg_set_diag", "msg_set_speculative",
     "msg_set_fast_commit",
-    "msg_set_batch_inflight", "msg_set_batch_floods", "msg_set_resolve_grid", "msg_watershed_colorize_batch_dev",
+    "msg_set_batch_inflight", "msg_set_batch_floods", "msg_set_batch_devices", "msg_set_resolve_grid", "msg_watershed_colorize_batch_dev",
     "msg_gray_hist_dev", "msg_nc_levels", "msg_nc_marker_lut", "msg_nc_markers_dev",
     "msg_nc_marker_stage_dev", "msg_nc_marker_stage",
     "msg_blur_mask_size", "msg_shape_markers_dev", "msg_shape_markers",
@@ -176,6 +176,9 @@ def load():
     if hasattr(L, "msg_set_batch_floods"):  # (MSEGMENT_LIB A/B builds of earlier rounds lack it)
         L.msg_set_batch_floods.argtypes = [vp, i]
         L.msg_set_batch_floods.restype = i
+    if hasattr(L, "msg_set_batch_devices"):  # (ABI 7)
+        L.msg_set_batch_devices.argtypes = [vp, i, vp]
+        L.msg_set_batch_devices.restype = i
     L.msg_set_resolve_grid.argtypes = [vp, i]
     L.msg_set_resolve_grid.restype = i
     L.msg_watershed_colorize_batch_dev.argtypes = [vp, i, vp, vp, vp, vp, vp, i, vp, vp, vp]

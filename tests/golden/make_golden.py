@@ -117,8 +117,9 @@ DIGEST_CASES = [("mosaic", 1024, 1024, 1), ("mosaic_noise", 1024, 1024, 1),
                 ("mosaic", 4096, 4096, 100), ("mosaic", 3001, 5003, 7),
                 ("mosaic_noise", 4096, 4096, 2), ("random", 4096, 4096, 2),
                 ("mosaic", 16387, 32749, 11)]  # above 2^28 pixels, ragged tiles: the flood's size limit
-# config 5's other frames as bench.py times them (seeds 100 + k, k = 1..7: one batch of 8)
-DIGEST_CASES += [("mosaic", 4096, 4096, 100 + k) for k in range(1, 8)]
+# config 5's other 63 frames (seeds 100 + k, k = 1..63: SURVEY 8d; bench.py --gpus N gives rank r
+# the batch of frames 100 + 8r .. 100 + 8r + 7, so all 64 are checked at N = 8)
+DIGEST_CASES += [("mosaic", 4096, 4096, 100 + k) for k in range(1, 64)]
 
 
 def write_digests(only=None):

@@ -4,7 +4,8 @@
 // the shim never holds one across a library call.
 //   mock_env validate            -- argument checks only (no GPU): every bad call -> MSG_EINVAL
 //   mock_env run <in> <out>      -- one watershedColorize through the shim on GPU 0
-//   mock_env batch <mode> <in> <out> -- watershedColorizeBatch of the frames in <in> (batch floods mode)
+//   mock_env batch <mode> <in> <out> [d0,d1,..] -- watershedColorizeBatch of the frames in <in> (batch
+//                                    floods mode), optionally spread over a device list (setBatchDevices)
 #include <jni.h>
 
 #include <cstdio>
@@ -26,6 +27,7 @@ jint Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_shapeMarkers(JNI
 jint Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_colorMarkers(JNIEnv*, jclass, jlong, jbyteArray,
                                                                              jint, jint, jbyteArray, jintArray);
 jint Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_setBatchFloods(JNIEnv*, jclass, jlong, jint);
+jint Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_setBatchDevices(JNIEnv*, jclass, jlong, jintArray);
 jint Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_watershedColorizeBatch(
     JNIEnv*, jclass, jlong, jobjectArray, jobjectArray, jintArray, jintArray, jint, jbyteArray, jobjectArray);
 }
@@ -185,6 +187,13 @@ static int validate() {
   }
   expect(Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_setBatchFloods(&env, nullptr, 0, 1),
          "batch floods null ctx");
+  expect(Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_setBatchDevices(&env, nullptr, 0, ints_of({0})),
+         "batch devices null ctx");
+  expect(Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_setBatchDevices(&env, nullptr, fake, nullptr),
+         "batch devices null list");
+  expect(Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_setBatchDevices(&env, nullptr, fake,
+                                                                                     ints_of(std::vector<jint>(65, 0))),
+         "batch devices 65 entries");
   if (g_critical) {
     std::printf("FAIL critical regions taken: %d\n", g_critical);
     ++bad;
@@ -230,7 +239,7 @@ static int run(const char* in, const char* out) {
 
 // in: int32 n, depth, has_palette; [depth*3 palette bytes]; n x {int32 rows, cols; BGR bytes;
 // int32 markers}.  out: rc, then per frame the markers and the dst bytes.
-static int run_batch(int mode, const char* in, const char* out) {
+static int run_batch(int mode, const char* in, const char* out, const char* devs) {
   FILE* f = std::fopen(in, "rb");
   if (!f) return 2;
   int32_t hdr[3];
@@ -259,6 +268,17 @@ static int run_batch(int mode, const char* in, const char* out) {
   JNIEnv env;
   const jlong cx = reinterpret_cast<jlong>(c);
   jint rc = Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_setBatchFloods(&env, nullptr, cx, mode);
+  if (rc == MSG_OK && devs) {  // "0,0": MSegmentNative.watershedBatch(..., new int[]{0, 0})
+    std::vector<jint> dv;
+    for (const char* p = devs; *p;) {
+      char* e = nullptr;
+      const long v = std::strtol(p, &e, 10);
+      if (e == p) break;
+      dv.push_back((jint)v);
+      p = (*e == ',') ? e + 1 : e;
+    }
+    rc = Java_ru_shayhulud_opencvcmsegment_nativeseg_MSegmentNative_setBatchDevices(&env, nullptr, cx, ints_of(dv));
+  }
   Objs* ob = objs(b);
   Objs* om = objs(m);
   Objs* od = objs(d);
@@ -280,7 +300,8 @@ static int run_batch(int mode, const char* in, const char* out) {
 int main(int argc, char** argv) {
   if (argc >= 2 && std::string(argv[1]) == "validate") return validate();
   if (argc >= 4 && std::string(argv[1]) == "run") return run(argv[2], argv[3]);
-  if (argc >= 5 && std::string(argv[1]) == "batch") return run_batch(std::atoi(argv[2]), argv[3], argv[4]);
-  std::fprintf(stderr, "usage: mock_env validate | run <in> <out> | batch <mode> <in> <out>\n");
+  if (argc >= 5 && std::string(argv[1]) == "batch")
+    return run_batch(std::atoi(argv[2]), argv[3], argv[4], argc >= 6 ? argv[5] : nullptr);
+  std::fprintf(stderr, "usage: mock_env validate | run <in> <out> | batch <mode> <in> <out> [devices]\n");
   return 2;
 }

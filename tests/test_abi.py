@@ -26,7 +26,7 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_binding_load():
     L = _lib.load()
-    assert L.msg_abi_version() == 6
+    assert L.msg_abi_version() == 7
 
 
 def test_build_id_matches_sources():

@@ -1,6 +1,7 @@
 """CPU, world_size 2 over gloo: bench.py's multi-rank harness (barriers around exactly K steps,
-max-over-ranks timing, whole-job Mpx/s).  The data path itself has no collectives (replicas:
-one frame per GPU), so the only distributed logic to prove is the timing/aggregation."""
+max-over-ranks timing, whole-job Mpx/s, the per-rank config-5 frame blocks and the summed digest
+parity).  The data path itself has no collectives (replicas: 8 frames per GPU), so the only
+distributed logic to prove is the frame assignment, the timing and the aggregation."""
 import os
 import socket
 import sys
@@ -89,13 +90,15 @@ def test_bench_gpus_flag_spawns_ranks():
 
 
 def _replica_worker(rank, world, port, q):
-    """One rank of bench.py's N > 1 layout on CPU: the frame frame_seed gives this rank (config 5's
-    100 + rank), flooded by the C oracle as the stand-in for the GPU step; the labels' digest is
-    gathered to rank 0 -- the only exchange, the data path itself has none."""
+    """One rank of bench.py's N > 1 layout on CPU: the frames bench.default_frames / frame_seed give
+    this rank (config 5's 100 + 8r .. 100 + 8r + 7), flooded by the C oracle as the stand-in for the
+    GPU batch step, checked against the committed digests with bench.digest_parity and summed over
+    the ranks with bench.reduce_sum_ints -- the parity count bench.py prints; the data path itself
+    has no exchange."""
     sys.path[:0] = [ROOT, os.path.join(ROOT, "opencv-msegment_amd")]
-    import hashlib
+    import json
+    from concurrent.futures import ThreadPoolExecutor
 
-    import torch
     import torch.distributed as dist
 
     import bench
@@ -105,37 +108,42 @@ def _replica_worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    seed = bench.frame_seed(None, rank, world)
-    img, m, _ = synth.frame("mosaic", 4096, 4096, seed)
-    h = hashlib.sha256(ws_oracle.watershed(img, m).tobytes()).hexdigest()
-    mine = torch.tensor(list(bytes.fromhex(h)) + [seed], dtype=torch.int64)
-    got = [torch.zeros_like(mine) for _ in range(world)]
-    dist.all_gather(got, mine)
-    if rank == 0:
-        q.put([(int(t[-1]), bytes(t[:-1].tolist()).hex()) for t in got])
+    K = bench.default_frames(None, world)
+    seed = bench.frame_seed(None, rank, world, K)
+    seeds = list(range(seed, seed + K))
+
+    def flood(s):  # the oracle runs without the GIL inside ctypes
+        img, m, _ = synth.frame("mosaic", 4096, 4096, s)
+        return ws_oracle.watershed(img, m)
+
+    with ThreadPoolExecutor(4) as ex:
+        labs = list(ex.map(flood, seeds))
+    dgs = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
+    mine = bench.digest_parity(labs, ["mosaic_4096x4096_s%d" % s for s in seeds], dgs)
+    total = bench.reduce_sum_ints(mine)
+    q.put((rank, seeds, mine, total))
     dist.barrier()
     dist.destroy_process_group()
 
 
 def test_two_rank_replicas_segment_their_own_config5_frames():
-    """world size 2: rank r floods config 5's frame 100 + r (bench.frame_seed), each digest equals
-    the committed oracle digest of that frame, and the two ranks did different frames."""
-    import json
-
+    """world size 2: rank r floods config 5's frames 100 + 8r .. 100 + 8r + 7 (bench.py's default
+    N > 1 step), every label map equals the committed oracle digest of its frame, the two ranks did
+    different frames, and the summed parity count is 16/16."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_replica_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = q.get(timeout=300)
+    res = sorted(q.get(timeout=600) for _ in procs)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    dgs = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
-    assert [s for s, _ in res] == [100, 101]
-    for seed, h in res:
-        assert h == dgs["mosaic_4096x4096_s%d" % seed]["labels_sha256"], seed
+    (r0, s0, m0, t0), (r1, s1, m1, t1) = res
+    assert s0 == list(range(100, 108)) and s1 == list(range(108, 116))
+    assert tuple(m0) == tuple(m1) == (8, 0)
+    assert t0 == t1 == [16, 0]
 
 
 def test_bench_rejects_gpus_world_mismatch():

@@ -198,6 +198,38 @@ def test_config5_frames_batch_vs_digest(seg):
         assert hashlib.sha256(got.tobytes()).hexdigest() == dgs["mosaic_4096x4096_s%d" % (100 + k)]["labels_sha256"], k
 
 
+def test_config5_multi_device_batch_vs_digest(seg):
+    """Config 5 through the multi-device C-ABI entry (msg_set_batch_devices) as the JVM reaches it:
+    the device list [0, 0] (two sub-contexts on the one GPU of the box, 4 frames each, each with its
+    own floods in flight), host buffers, colorByIndexes; all 8 frames against the oracle digests,
+    the colours against the oracle's colouring of the digest-checked labels; then a bad list and
+    the reset to the context's own device."""
+    import msegment
+
+    dgs = json.load(open(os.path.join(GOLD, "digests.json")))
+    fr = [synth.frame("mosaic", 4096, 4096, 100 + k) for k in range(8)]
+    depth = max(f[2] for f in fr)
+    work = [(f[0], f[1].copy()) for f in fr]
+    seg.set_batch_devices([0, 0])
+    try:
+        dsts = seg.watershed_batch(work, depth=depth)
+        st = seg.stats()
+        with pytest.raises(msegment.MsegError):
+            seg.set_batch_devices([0, 4096])
+    finally:
+        seg.set_batch_devices([])
+    assert st["rows"] == 4096 and st["pops"] > 8 * 4000 * 4000  # the sums over both sub-contexts
+    for k, (_, lab) in enumerate(work):
+        assert hashlib.sha256(lab.tobytes()).hexdigest() == dgs["mosaic_4096x4096_s%d" % (100 + k)]["labels_sha256"], k
+    for k in (0, 7):  # first frame of each block
+        assert np.array_equal(dsts[k], ws_oracle.colorize(work[k][1], depth, None)), k
+    # back on the context's own device
+    img, m, _ = synth.frame("mosaic_noise", 96, 80, 5)
+    w2 = [(img, m.copy())]
+    seg.watershed_batch(w2)
+    assert np.array_equal(w2[0][1], ws_oracle.watershed(img, m))
+
+
 def check_properties(m, out):
     """Size-independent watershed invariants."""
     H, W = m.shape

@@ -53,3 +53,35 @@ def test_product_package_never_imports_oracle():
             if f.endswith((".py", ".hip", ".cpp", ".h")):
                 src = open(os.path.join(dp, f), encoding="utf-8", errors="replace").read()
                 assert "ws_oracle" not in src and "ws_pyref" not in src and "liboracle" not in src, f
+
+
+def _unbound_segmenter():
+    """A Segmenter whose context was never created (no GPU here): any call that reached the library
+    would fail on the null handle, so an MsegError(MSG_EINVAL) raised here comes from the binding's
+    own argument checks."""
+    import msegment
+    from msegment import _lib
+
+    s = msegment.Segmenter.__new__(msegment.Segmenter)
+    s._L = _lib.load()
+    s._h = None
+    s.device = 0
+    return s
+
+
+def test_batch_rejects_short_palette_and_size_mismatch():
+    import pytest
+
+    from msegment import MsegError, _lib
+
+    seg = _unbound_segmenter()
+    img, m, _ = synth.frame("mosaic", 16, 24, 1)
+    with pytest.raises(MsegError) as e:  # 4 colours needed, 3 given: C would read past the buffer
+        seg.watershed_batch([(img, m.copy())], depth=4, palette=np.zeros((3, 3), np.uint8))
+    assert e.value.code == _lib.MSG_EINVAL and "palette" in str(e.value)
+    with pytest.raises(MsegError) as e:  # rows and cols come from the markers: the image must agree
+        seg.watershed_batch([(img[:15], m.copy())], depth=4)
+    assert e.value.code == _lib.MSG_EINVAL and "sizes differ" in str(e.value)
+    with pytest.raises(MsegError) as e:
+        seg.watershed_batch([(img, m.astype(np.int64))])
+    assert e.value.code == _lib.MSG_EINVAL

@@ -64,11 +64,13 @@ def test_jni_shim_watershed_on_gpu(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [0, 1])
-def test_jni_shim_batch_on_gpu(tmp_path, mode):
+@pytest.mark.parametrize("mode,devs", [(0, None), (1, None), (0, "0,0"), (1, "0,0")])
+def test_jni_shim_batch_on_gpu(tmp_path, mode, devs):
     """MSegmentNative.watershedColorizeBatch through the shim: CorrelationTestService's many floods
     per image (CorrelationTestService.java:84-86, 141 -> PictureService.java:852) handed over in one
-    call, in the default batch path (mode 0) and the many-floods mode (mode 1)."""
+    call, in the default batch path (mode 0) and the many-floods mode (mode 1); with devs, spread
+    over the device list {0, 0} first (MSegmentNative.watershedBatch(..., devices) ->
+    setBatchDevices -> msg_set_batch_devices: two sub-contexts, frames 0-1 and 2-4)."""
     from msegment import synth
     from msegment.jrandom import generate_bgr_palette
     from oracle import ws_oracle
@@ -90,7 +92,8 @@ def test_jni_shim_batch_on_gpu(tmp_path, mode):
             f.write(struct.pack("<2i", *m.shape))
             f.write(img.tobytes())
             f.write(m.tobytes())
-    r = subprocess.run([exe, "batch", str(mode), src, dst], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, "batch", str(mode), src, dst] + ([devs] if devs else []), capture_output=True,
+                       text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     raw = open(dst, "rb").read()
     assert struct.unpack("<i", raw[:4])[0] == 0
