@@ -77,13 +77,14 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")  # scripts/pmc_s
 E2E_BYTES_PER_PIXEL = 14.0                  # 3 B BGR + 4 B markers in, 4 B labels + 3 B BGR out
 
 
-def frame_seed(seed, rank, world, frames=1):
-    """The first frame a rank segments: --seed, else config 3's seed 2 on one GPU, else config 5's
-    frame 100 + frames * rank (config 5's frames are 100 + k, k = 0..63; with 8 frames
+def frame_seed(seed, rank, world, frames=1, size=4096):
+    """The first frame a rank segments: --seed, else on one GPU SURVEY 8d's seed of the config that
+    size is (config 2's 1024^2 seed 1, config 3's 4096^2 seed 2, config 4's 16384^2 seed 3), else
+    config 5's frame 100 + frames * rank (config 5's frames are 100 + k, k = 0..63; with 8 frames
     per rank, rank r takes 100 + 8r .. 100 + 8r + 7; replicas, no collectives)."""
     if seed is not None:
         return seed
-    return 2 if world == 1 else 100 + frames * rank
+    return {1024: 1, 16384: 3}.get(size, 2) if world == 1 else 100 + frames * rank
 
 
 def default_frames(frames, world):
@@ -765,7 +766,7 @@ def main(argv=None):
 
     S = args.size
     K = default_frames(args.frames, world)
-    seed = frame_seed(args.seed, rank, world, K)
+    seed = frame_seed(args.seed, rank, world, K, S)
     # the workload the PMC passes must have been collected on for their traffic to be quoted
     pmc_cfg = {"pipeline": args.pipeline, "kind": args.kind, "size": S, "seed": seed, "frames": K}
     t0 = time.perf_counter()
@@ -832,7 +833,12 @@ def main(argv=None):
             seg.watershed_colorize_dev(t_sharp, t_lab, t_lab, d, None, t_dst)
 
         step = step1
-    MARKERS = NC or SHAPE or COLOR  # a marker stage before the flood: no digest, no side lines
+    MARKERS = NC or SHAPE or COLOR  # a marker stage before the flood: the pipeline's digest, no side lines
+    pipe_key = None
+    if NC:
+        pipe_key = "nc_%s_%dx%d_s%d_d%d_%s" % (args.kind, S, S, seed, args.nc_depth, "+".join(nc_opts) or "none")
+    elif SHAPE or COLOR:
+        pipe_key = "%s_%s_%dx%d_s%d" % (args.pipeline, args.kind, S, S, seed)
 
     for _ in range(args.warmup):
         step()
@@ -841,6 +847,12 @@ def main(argv=None):
     parity = None
     dgs = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
     dkey = "%s_%dx%d_s%d" % (args.kind, S, S, seed)
+    if MARKERS and dgs.get(pipe_key):
+        # the marker-stage pipeline's frame against the oracle digest of the whole pipeline
+        # (tests/golden/make_golden.py --pipelines: numpy marker stage + the C flood)
+        got = hashlib.sha256(t_lab.cpu().numpy().tobytes()).hexdigest()
+        parity = ("bit-exact vs oracle digest" if got == dgs[pipe_key]["labels_sha256"]
+                  else "MISMATCH vs oracle digest") + " " + pipe_key
     if not MARKERS:
         # every rank: each of its K label maps against its committed oracle digest, summed over ranks
         keys = ["%s_%dx%d_s%d" % (args.kind, S, S, seed + k) for k in range(K)]
@@ -852,8 +864,8 @@ def main(argv=None):
                 parity = ("bit-exact vs oracle digest" if not bad else "MISMATCH vs oracle digest") + " " + dkey
         elif checked:
             parity = "%d/%d frames bit-exact vs oracle digests (%s frames %d..%d over %d rank%s)" % (
-                checked - bad, checked, args.kind, frame_seed(args.seed, 0, world, K),
-                frame_seed(args.seed, world - 1, world, K) + K - 1, world, "s" if world > 1 else "")
+                checked - bad, checked, args.kind, frame_seed(args.seed, 0, world, K, S),
+                frame_seed(args.seed, world - 1, world, K, S) + K - 1, world, "s" if world > 1 else "")
         if rank == 0:
             log("[rank 0] parity:", parity)
 

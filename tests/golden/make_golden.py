@@ -15,7 +15,8 @@ pipeline and real-image flood timing (scripts/real_image_probe.py, tests/test_gp
 
 Outputs (numpy .npz, no pickles):
   small_cases.npz  inputs + expected labels + expected colourised/gray outputs, small frames
-  digests.json     SHA-256 of the oracle's label maps for larger synthetic frames
+  digests.json     SHA-256 of the oracle's label maps for larger synthetic frames, and of the
+                   marker-stage pipelines' 4096^2 frames (--pipelines)
 """
 import hashlib
 import json
@@ -105,6 +106,7 @@ def main():
     np.savez_compressed(os.path.join(OUT, "small_cases.npz"), **arrays)
 
     write_digests()
+    write_pipeline_digests()
     print("wrote", len(names), "small cases")
 
 
@@ -145,6 +147,45 @@ def write_digests(only=None):
         json.dump(digests, f, indent=1, sort_keys=True)
 
 
+# The marker-stage pipelines' 4096^2 frames as bench.py --pipeline nc / shape / color time them
+# (mosaic seed 2; nc: depth 4, GISTO_DIAP): the numpy restatements of the marker stages
+# (oracle/nc_oracle.py, shape_oracle.py, color_oracle.py) then the C flood.  ~1 min in all.
+PIPELINE_CASES = [("nc", "mosaic", 4096, 2, 4, "GISTO_DIAP"), ("shape", "mosaic", 4096, 2, None, None),
+                  ("color", "mosaic", 4096, 2, None, None)]
+
+
+def pipeline_key(pipe, kind, S, seed, depth=None, opts=None):
+    if pipe == "nc":
+        return "nc_%s_%dx%d_s%d_d%d_%s" % (kind, S, S, seed, depth, opts or "none")
+    return "%s_%s_%dx%d_s%d" % (pipe, kind, S, S, seed)
+
+
+def write_pipeline_digests():
+    from oracle import color_oracle, nc_oracle, shape_oracle
+
+    path = os.path.join(OUT, "digests.json")
+    digests = json.load(open(path))
+    for pipe, kind, S, seed, depth, opts in PIPELINE_CASES:
+        img, _, _ = synth.frame(kind, S, S, seed)
+        src, extra = img, {}
+        if pipe == "nc":
+            _, _, lv, mk = nc_oracle.marker_stage(img, depth, gisto_diap="GISTO_DIAP" in (opts or ""))
+            d = len(lv)
+        elif pipe == "shape":
+            mk, d = shape_oracle.shape_markers(img, shape_oracle.blur_mask_size(S, S))
+        else:
+            src, mk, d = color_oracle.color_markers(img)
+            extra["sharp_sha256"] = hashlib.sha256(src.tobytes()).hexdigest()
+        lab = ws_oracle.watershed(src, mk)
+        key = pipeline_key(pipe, kind, S, seed, depth, opts)
+        digests[key] = dict(extra, labels_sha256=hashlib.sha256(lab.tobytes()).hexdigest(),
+                            markers_sha256=hashlib.sha256(np.ascontiguousarray(mk, np.int32).tobytes()).hexdigest(),
+                            depth=int(d), wshed_pixels=int((lab == -1).sum()), zero_pixels=int((lab == 0).sum()))
+        print(key, digests[key]["labels_sha256"][:16], "depth", d)
+    with open(path, "w") as f:
+        json.dump(digests, f, indent=1, sort_keys=True)
+
+
 def write_album():
     """The reference's resource images, decoded by PIL (RGB, palette expanded) and re-encoded
     losslessly: the decoded pixels are the fixture (data), not the decoder."""
@@ -162,6 +203,8 @@ def write_album():
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--album":
         write_album()
+    elif len(sys.argv) > 1 and sys.argv[1] == "--pipelines":
+        write_pipeline_digests()
     elif len(sys.argv) > 1 and sys.argv[1] == "--digests-only":  # e.g. --digests-only mosaic_16384x16384_s3
         write_digests(set(sys.argv[2:]) or None)
     else:

@@ -85,3 +85,17 @@ def test_batch_rejects_short_palette_and_size_mismatch():
     with pytest.raises(MsegError) as e:
         seg.watershed_batch([(img, m.astype(np.int64))])
     assert e.value.code == _lib.MSG_EINVAL
+
+
+def test_nc_pipeline_digest_reproduces():
+    """The committed digest the NC pipeline's bench line is checked against
+    (make_golden.py --pipelines) is what the oracles produce on that frame today."""
+    from oracle import nc_oracle, ws_oracle
+
+    with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+        dg = json.load(f)["nc_mosaic_4096x4096_s2_d4_GISTO_DIAP"]
+    img, _, _ = synth.frame("mosaic", 4096, 4096, 2)
+    _, _, lv, mk = nc_oracle.marker_stage(img, 4, gisto_diap=True)
+    assert len(lv) == dg["depth"]
+    assert hashlib.sha256(np.ascontiguousarray(mk, np.int32).tobytes()).hexdigest() == dg["markers_sha256"]
+    assert hashlib.sha256(ws_oracle.watershed(img, mk).tobytes()).hexdigest() == dg["labels_sha256"]
