@@ -25,8 +25,11 @@ and side lines that are parity cases, not the headline: "batch" (BASELINE config
 frames per call, digest-checked), "stress" / "stress_random" (config 3's mosaic+noise and uniform
 random variants, digest-checked, 1-core oracle beside them), "many_floods" (1024
 notConnectedMarkers floods of 1024^2 per call in the many-floods mode, every frame checked
-against the oracle, 16-thread oracle beside it; --many-frames), "colour_distance" (the stand-alone
-L-inf stencil against the HBM roofline).
+against the oracle, 16-thread oracle beside it; --many-frames), "correlation" (the reference's own
+flood pattern: CorrelationTestService's 92 floods of ONE image per call -- 90 notConnectedMarkers
+marker maps, the shape and the colour method's -- on a 1024^2 synthetic frame and on album.jpg,
+every flood checked against the oracle, 16-thread oracle beside it; --correlation),
+"colour_distance" (the stand-alone L-inf stencil against the HBM roofline).
 """
 import argparse
 import hashlib
@@ -447,21 +450,27 @@ def many_floods_line(seg, sync, dev, K, S=1024, steps=2, cpu=True, nc_depth=4):
         sync()
         dt = time.perf_counter() - t0
     finally:
-        seg.set_batch_floods(0)
+        seg.set_batch_floods(0)  # releases the mode's workspaces; then back to the default (automatic)
+        seg.set_batch_floods(3)
     st = seg.stats()
     out = {"workload": "%d notConnectedMarkers floods (mosaic_noise %dx%d seeds 100..%d, GISTO_DIAP depth %d "
                        "markers) + colorByIndexes per batch call, device-resident, many-floods mode"
                        % (K, S, S, 99 + K, nc_depth),
            "value": round(K * S * S * steps / dt / 1e6, 3), "unit": "Mpx/s", "steps": steps,
            "ms_per_step": round(1000.0 * dt / steps, 3), "pops_per_step": st["pops"]}
-    # the default batch path on the first 8 frames (the full engine per flood, 4 streams in flight)
+    # the full engine per flood (mode 0, 4 streams in flight) on the first 8 frames
     k8 = min(8, K)
     seg.set_batch_inflight(4)
-    t0 = time.perf_counter()
-    seg.watershed_colorize_batch_dev(imgs[:k8], mks[:k8], labs[:k8], depth, None, dsts[:k8])
-    sync()
-    out["default_batch_path"] = {"value": round(k8 * S * S / (time.perf_counter() - t0) / 1e6, 3),
-                                 "unit": "Mpx/s", "frames": k8, "inflight": 4}
+    seg.set_batch_floods(0)
+    try:
+        t0 = time.perf_counter()
+        seg.watershed_colorize_batch_dev(imgs[:k8], mks[:k8], labs[:k8], depth, None, dsts[:k8])
+        sync()
+        out["mode0_batch_path"] = {"value": round(k8 * S * S / (time.perf_counter() - t0) / 1e6, 3),
+                                   "unit": "Mpx/s", "frames": k8, "inflight": 4,
+                                   "note": "msg_set_batch_floods 0: the full engine per flood"}
+    finally:
+        seg.set_batch_floods(3)
     if cpu:
         from oracle import ws_oracle
 
@@ -483,6 +492,143 @@ def many_floods_line(seg, sync, dev, K, S=1024, steps=2, cpu=True, nc_depth=4):
         bad = sum(not np.array_equal(labs[k].cpu().numpy(), want[k]) for k in range(K))
         out["parity"] = "%d/%d frames bit-exact vs the C oracle" % (K - bad, K)
     del imgs, mks, labs, dsts
+    return out
+
+
+# CorrelationTestService.test (CorrelationTestService.java:28-40, 84-99): per image, the colour and
+# shape methods once and notConnectedMarkers for every depth x mask size x option set -- 92 floods
+# of ONE image per test, each through PictureService.watershed (PictureService.java:378, 455, 852)
+CORR_DEPTHS = (2, 3, 4, 5, 6)
+CORR_MASKS = (3, 5, 7)
+CORR_OPTS = (("MEDIAN_BLUR",), ("MEDIAN_BLUR", "GISTO_DIAP"), ("BILATERIAL",), ("BILATERIAL", "GISTO_DIAP"),
+             (), ("GISTO_DIAP",))
+NC_FLAG = {"GISTO_DIAP": 0x1, "MULTI_OTSU": 0x2, "MEDIAN_BLUR": 0x4, "BILATERIAL": 0x8}
+
+
+def correlation_image(name):
+    """The image of the correlation line: 'album' = the reference's own album.jpg (1500^2, decoded
+    pixels in tests/golden/album_1500x1500.png), else a synthetic 1024^2 frame of that kind."""
+    import numpy as np
+
+    from msegment import synth
+
+    if name == "album":
+        from PIL import Image
+
+        rgb = np.asarray(Image.open(os.path.join(ROOT, "tests", "golden", "album_1500x1500.png")).convert("RGB"))
+        return np.ascontiguousarray(rgb[:, :, ::-1]), "album.jpg 1500x1500 (tests/golden)"
+    return synth.frame(name, 1024, 1024, 100)[0], "%s 1024x1024 seed 100" % name
+
+
+def correlation_line(seg, sync, dev, name, cpu=True, steps=2):
+    """The reference's real call pattern for the flood: CorrelationTestService floods ONE image 92
+    times per test -- 90 notConnectedMarkers marker maps (5 depths x 3 mask sizes x 6 option sets),
+    the shape method's and the colour method's (whose flood source is the sharpened image).  The
+    marker maps come from the GPU marker stages (outside the timed region); each step is ONE batch
+    call of the 92 floods + colorByIndexes in the many-floods mode (msg_set_batch_floods 1), the
+    default batch path (full engine per flood, 4 in flight) timed once beside it, and the C oracle
+    over the same 92 floods on the host's threads, whose labels are the parity check."""
+    import numpy as np
+    import torch
+
+    img, desc = correlation_image(name)
+    H, W = img.shape[:2]
+    t_img = torch.from_numpy(img).to(dev)
+    srcs, mks, depths, names = [], [], [], []
+    for depth in CORR_DEPTHS:
+        for mask in CORR_MASKS:
+            for opts in CORR_OPTS:
+                m = torch.empty((H, W), dtype=torch.int32, device=dev)
+                flags = sum(NC_FLAG[o] for o in opts) | ((mask & 0xff) << 8)
+                lv = seg.nc_marker_stage_dev(t_img, depth, m, flags)
+                srcs.append(t_img)
+                mks.append(m)
+                depths.append(len(lv))
+                names.append("NC,%d,%d,%s" % (depth, mask, "-".join(opts)))
+    m = torch.empty((H, W), dtype=torch.int32, device=dev)
+    d, _ = seg.shape_markers_dev(t_img, m)
+    srcs.append(t_img)
+    mks.append(m)
+    depths.append(d)
+    names.append("SHAPE")
+    t_sharp = torch.empty_like(t_img)
+    m = torch.empty((H, W), dtype=torch.int32, device=dev)
+    depths.append(seg.color_markers_dev(t_img, t_sharp, m))
+    srcs.append(t_sharp)
+    mks.append(m)
+    names.append("COLOR")
+    sync()
+    n = len(mks)
+    depth = max(depths)
+    labs = [torch.empty_like(x) for x in mks]
+    dsts = [torch.empty((H, W, 3), dtype=torch.uint8, device=dev) for _ in mks]
+    seg.set_batch_floods(1)
+    try:
+        seg.watershed_colorize_batch_dev(srcs, mks, labs, depth, None, dsts)  # warm-up (workspaces)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            seg.watershed_colorize_batch_dev(srcs, mks, labs, depth, None, dsts)
+        sync()
+        dt = time.perf_counter() - t0
+    finally:
+        seg.set_batch_floods(0)
+        seg.set_batch_floods(3)
+    st = seg.stats()
+    out = {"workload": "CorrelationTestService.test's %d floods of ONE image (%s): 90 notConnectedMarkers "
+                       "marker maps (depths 2-6 x masks 3,5,7 x 6 option sets), the shape and the colour "
+                       "method's, + colorByIndexes, one batch call, device-resident, many-floods mode"
+                       % (n, desc),
+           "value": round(n * H * W * steps / dt / 1e6, 3), "unit": "Mpx/s", "floods": n, "steps": steps,
+           "ms_per_step": round(1000.0 * dt / steps, 3), "pops_per_step": st["pops"]}
+    # the library's default (msg_set_batch_floods 3, automatic): the first call of a frame size
+    # floods frame 0 alone as a probe and picks the path for the rest; the second call reuses it
+    seg.set_batch_inflight(4)
+    auto = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        seg.watershed_colorize_batch_dev(srcs, mks, labs, depth, None, dsts)
+        sync()
+        sa = seg.stats()
+        auto.append({"value": round(n * H * W / (time.perf_counter() - t0) / 1e6, 3), "unit": "Mpx/s",
+                     "batch_mode": sa["batch_mode"], "probe": bool(sa["batch_probe"])})
+    out["default_path"] = {"first_call": auto[0], "second_call": auto[1],
+                           "note": "msg_set_batch_floods 3 (the default): frame 0 probed alone on the first call"}
+    # the full engine per flood (mode 0, 4 in flight) on the first 8 floods
+    seg.set_batch_floods(0)
+    try:
+        t0 = time.perf_counter()
+        seg.watershed_colorize_batch_dev(srcs[:8], mks[:8], labs[:8], depth, None, dsts[:8])
+        sync()
+        out["mode0_batch_path"] = {"value": round(8 * H * W / (time.perf_counter() - t0) / 1e6, 3), "unit": "Mpx/s",
+                                   "floods": 8, "inflight": 4, "note": "msg_set_batch_floods 0, the first 8 floods"}
+    finally:
+        seg.set_batch_floods(3)
+    if cpu:
+        from concurrent.futures import ThreadPoolExecutor
+
+        from oracle import ws_oracle
+
+        nt = batch_cpu_threads(n)
+        src_host = {id(x): x.cpu().numpy() for x in (t_img, t_sharp)}
+        m_host = [x.cpu().numpy() for x in mks]
+
+        def one(k):
+            lab = ws_oracle.watershed(src_host[id(srcs[k])], m_host[k])
+            ws_oracle.colorize(lab, depth, None)
+            return lab
+
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(nt) as ex:
+            want = list(ex.map(one, range(n)))
+        cdt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(n * H * W / cdt / 1e6, 3), "unit": "Mpx/s", "cores": nt, "kind": "port",
+                               "sample": "the same %d floods (the GPU's marker maps), one flood per thread: "
+                                         "oracle/ws_oracle.c watershed + colorize, %.2f s" % (n, cdt)}
+        bad = [names[k] for k in range(n) if not np.array_equal(labs[k].cpu().numpy(), want[k])]
+        out["parity"] = "%d/%d floods bit-exact vs the C oracle%s" % (n - len(bad), n,
+                                                                    (" (differ: %s)" % bad[:4]) if bad else "")
+    del srcs, mks, labs, dsts, t_img, t_sharp
     return out
 
 
@@ -717,6 +863,9 @@ def main(argv=None):
                     help="steps of the config-3 stress line (mosaic+noise at --size); 0 = skip")
     ap.add_argument("--many-frames", type=int, default=1024,
                     help="frames of the many-floods line (0: skip it)")
+    ap.add_argument("--correlation", default="mosaic_noise,album",
+                    help="images of the correlation line (CorrelationTestService's 92 floods of one image "
+                         "per call): comma list of mosaic_noise / random / mosaic (1024^2) / album; '' = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile-pass", action="store_true")
     ap.add_argument("--batch-only", action="store_true", help=argparse.SUPPRESS)
@@ -903,6 +1052,12 @@ def main(argv=None):
     if rank == 0 and world == 1 and K == 1 and not MARKERS and args.kind == "mosaic" and args.many_frames > 0:
         many = many_floods_line(seg, sync, dev, args.many_frames, cpu=not args.no_cpu_baseline)
 
+    corr = None
+    if rank == 0 and world == 1 and K == 1 and not MARKERS and args.kind == "mosaic" and args.correlation:
+        corr = {}
+        for name in args.correlation.split(","):
+            corr[name] = correlation_line(seg, sync, dev, name, cpu=not args.no_cpu_baseline)
+
     stress = stress_random = None
     if rank == 0 and world == 1 and K == 1 and not MARKERS and args.kind == "mosaic" and args.stress_steps > 0:
         stress = stress_line(seg, S, sync, dev, args.stress_steps, cpu=not args.no_cpu_baseline)
@@ -979,6 +1134,7 @@ def main(argv=None):
             "stress": stress,
             "stress_random": stress_random,
             "many_floods": many,
+            "correlation": corr,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
             "e2e_hbm": {"achieved": round(e2e_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

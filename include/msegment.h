@@ -91,6 +91,10 @@ typedef struct msg_stats {
     int64_t spec_exec_pops;     /* pops k_spec_round ran pop by pop: the top pops and cascade pops
                                    of every execution that was not replayed, over all rounds     */
     int64_t spec_longest_pops;  /* sum over the rounds of each round's longest such execution    */
+    /* batch calls (ABI 7) */
+    int64_t batch_mode;         /* the path the last batch call's frames took: 0 the full engine per
+                                   flood, 1 / 2 the many-floods kernel (msg_set_batch_floods)     */
+    int64_t batch_probe;        /* 1: mode 3 flooded frame 0 alone first to choose that path     */
 } msg_stats;
 
 #define MSG_NKERNELS 24
@@ -208,10 +212,20 @@ int msg_set_batch_devices(msg_ctx* ctx, int ndev, const int* devices);
  * CorrelationTestService.java:84-86, 141): every frame of the call gets a workspace of its own
  * (~44 B/px of HBM each), and ONE kernel pops all of them, one wave per flood, so the call keeps
  * as many floods in flight as it has frames instead of msg_set_batch_inflight's streams.
- *   mode 0: off (default: the full engine per flood, msg_set_batch_inflight of them at a time);
+ *   mode 0: off (the full engine per flood, msg_set_batch_inflight of them at a time);
  *   mode 1: every flood popped serially to its end in that kernel;
  *   mode 2: a flood that pops 4096 times in a row without pushing below its level (a plateau,
- *           where batches pay) is finished by the full engine instead.
+ *           where batches pay) is finished by the full engine instead;
+ *   mode 3: automatic (the default).  The first batch call of a frame size floods frame 0 alone
+ *           with the full engine (part of the call: its result is final) and prices the rest of
+ *           the batch both ways -- the full engine at that flood's wall time per flood,
+ *           msg_set_batch_inflight at a time, against the many-floods kernel at ~1 us per pop of
+ *           one wave with every flood in flight -- then runs the cheaper path (mode 0 or 1); later
+ *           calls of that frame size reuse the choice.  Plateaus and textures the speculative
+ *           engine serves (mosaic, noise) stay on the full engine; chains of dependent pops
+ *           (notConnectedMarkers' seeds, photographs) in batches larger than the floods in flight
+ *           go to the many-floods kernel.  If that kernel's workspaces do not fit the device, the
+ *           call falls back to mode 0.  msg_stats.batch_mode / batch_probe report what ran.
  * Results are identical in every mode (each is cv::watershed's exact serial order).
  * Memory: the per-frame workspaces stay allocated on the context between calls (the next call of
  * the same size reuses them) until mode 0 is set again, which releases them, or msg_destroy. */

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -98,7 +99,10 @@ struct msg_ctx {
   std::vector<msg_ctx*> subs;
   // many-floods batches (msg_set_batch_floods): one workspace per frame of the call, the Ws array
   // k_serial_multi reads, and the per-flood "still running" flags it leaves
-  int many = 0;                  // 0 off, 1 every flood serial to the end, 2 hand back to batches
+  int many = 3;                  // 0 off, 1 every flood serial to the end, 2 hand back to batches,
+                                 // 3 automatic (the default: choose_mode)
+  long long auto_key = -1;       // mode 3: frame size (rows << 32 | cols) the last probe was taken on
+  int auto_mode = -1;            //         and the mode it chose (0 or 1)
   std::vector<msg_ctx*> msubs;
   Ws* d_wss = nullptr;
   int wss_cap = 0;
@@ -803,6 +807,17 @@ int run_batch(msg_ctx* c, int n, F fn) {
   return MSG_OK;
 }
 
+// The many-floods mode's per-frame sub-contexts (~44 B/px each), Ws array and staging.
+void release_many(msg_ctx* c) {
+  for (msg_ctx* sub : c->msubs) msg_destroy(sub);
+  c->msubs.clear();
+  (void)hipSetDevice(c->dev);
+  dfree(c->d_wss);
+  c->wss_cap = 0;
+  dfree(c->d_mstage);
+  c->mstage_cap = 0;
+}
+
 // Many floods per launch (msg_set_batch_floods): every frame of the call gets a workspace of its
 // own (a sub-context), phase 1 of each is queued on its stream with k_scan's small-batch loop off
 // (FloodRun multi), then ONE k_serial_multi launch pops all of them, one wave per flood.  A flood
@@ -810,7 +825,7 @@ int run_batch(msg_ctx* c, int n, F fn) {
 // pops) is finished by the full engine, up to `inflight` at a time, speculative generations off.
 // frame(k, img, mk, H, W, lab, dst) describes frame k (device buffers; dst may be null).
 template <class F>
-int batch_many(msg_ctx* c, int n, int depth, const uint8_t* d_pal, F frame) {
+int batch_many(msg_ctx* c, int n, int mode, int depth, const uint8_t* d_pal, F frame) {
   if (n == 0) {
     c->stats = msg_stats{};
     return MSG_OK;
@@ -862,7 +877,7 @@ int batch_many(msg_ctx* c, int n, int depth, const uint8_t* d_pal, F frame) {
     h_ws[k] = frs[k].ws;
   }
   int rc = MSG_OK;
-  const int run_limit = c->many == 2 ? SERIAL_RUN : 0x7fffffff;
+  const int run_limit = mode == 2 ? SERIAL_RUN : 0x7fffffff;
   // the Ws array (copied before any launch reads it: hipMemcpyAsync from pageable memory returns
   // once the source is consumed), then one wave per flood once every phase 1 is queued before it
   if (hipMemcpyAsync(c->d_wss, h_ws.data(), (size_t)n * sizeof(Ws), hipMemcpyHostToDevice, c->own) != hipSuccess)
@@ -1434,6 +1449,27 @@ int host_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size_t* bgr_s
                const size_t* marker_stride, const int* rows, const int* cols, int depth, const uint8_t* palette,
                uint8_t* const* dst, const size_t* dst_stride);
 
+// msg_set_batch_floods mode 3 (automatic): which path a batch's frames take.  The regime of a flood
+// is only known by running it, so the first call for a frame size floods frame 0 alone with the full
+// engine on this context (a probe: its result is final, it is part of the call) and prices both paths
+// for the rest of the batch:
+//   full engine: the probe's wall time per flood, `inflight` floods overlapped at a time;
+//   many floods: every flood at once in one k_serial_multi launch, a serial pop per ~1 us of one
+//                wave, so about the probe's pop count in microseconds.
+// Interrupt-dense floods that the speculative engine serves well (noise) and plateaus (mosaic) price
+// far below their pop count and stay on the full engine; chains of dependent pops (notConnectedMarkers'
+// seeds, photographs) price at ~1 us per pop either way and go to the many-floods kernel once the batch
+// has more floods than in flight.  The choice is kept for that frame size (later calls skip the probe);
+// results are identical on either path.
+constexpr double AUTO_SERIAL_POP_US = 1.0;
+int auto_choice(const msg_ctx* c, int nrest, const msg_stats& probe, double probe_s) {
+  if (nrest <= 0) return 0;
+  const int k = std::max(1, std::min({c->inflight, nrest, MAX_INFLIGHT}));
+  const double full = probe_s * (double)((nrest + k - 1) / k);
+  const double many = 1e-6 * AUTO_SERIAL_POP_US * (double)probe.pops;
+  return many < full ? 1 : 0;
+}
+
 // msg_set_batch_devices: frames [n*j/D, n*(j+1)/D) on the sub-context of device-list entry j, one
 // host thread per entry, each a host_batch of its own (this context's batch settings copied over).
 // No data crosses devices: every block's buffers are the caller's host memory.
@@ -1499,6 +1535,10 @@ int spread_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size_t* bgr
   return MSG_OK;
 }
 
+int host_batch_mode(msg_ctx* c, int mode, int n, const uint8_t* const* bgr, const size_t* bgr_stride,
+                    int32_t* const* markers, const size_t* marker_stride, const int* rows, const int* cols, int depth,
+                    const uint8_t* palette, uint8_t* const* dst, const size_t* dst_stride);
+
 // The host-buffer batch (msg_watershed_batch, msg_watershed_colorize_batch): labels in place, and
 // the colourised frames when dst is given.  Many-floods mode: every frame staged (image, markers,
 // colour output, each 16-B aligned), flooded together, read back; otherwise run_batch.
@@ -1518,7 +1558,54 @@ int host_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size_t* bgr_s
   }
   if (!c->bdevs.empty() && n > 0)
     return spread_batch(c, n, bgr, bgr_stride, markers, marker_stride, rows, cols, depth, palette, dst, dst_stride);
-  if (!(c->many && n > 0))
+  int mode = c->many;
+  msg_stats pst{};
+  bool probed = false;
+  if (mode == 3) {  // automatic: the frame size's known choice, or a probe on frame 0 (auto_choice)
+    mode = 0;
+    const long long key = n > 0 ? ((long long)rows[0] << 32 | (unsigned)cols[0]) : -1;
+    if (n >= 2 && key == c->auto_key) {
+      mode = c->auto_mode;
+    } else if (n >= 2) {
+      const auto t0 = std::chrono::steady_clock::now();
+      const int rc = dst ? msg_watershed_colorize(c, bgr[0], bgr_stride[0], markers[0], marker_stride[0], rows[0],
+                                                  cols[0], depth, palette, dst[0], dst_stride[0], nullptr, 0)
+                         : msg_watershed(c, bgr[0], bgr_stride[0], markers[0], marker_stride[0], rows[0], cols[0]);
+      if (rc) return rc;
+      const double ps = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      pst = c->stats;
+      probed = true;
+      mode = auto_choice(c, n - 1, pst, ps);
+      c->auto_key = key;
+      c->auto_mode = mode;
+      ++bgr, ++bgr_stride, ++markers, ++marker_stride, ++rows, ++cols;  // the rest of the batch
+      if (dst) ++dst, ++dst_stride;
+      --n;
+    }
+  }
+  int rc = host_batch_mode(c, mode, n, bgr, bgr_stride, markers, marker_stride, rows, cols, depth, palette,
+                           dst, dst_stride);
+  if (rc == MSG_ENOMEM && c->many == 3 && mode != 0) {  // automatic choice without the memory: the full engine
+    release_many(c);
+    (void)hipGetLastError();
+    c->auto_mode = mode = 0;
+    rc = host_batch_mode(c, 0, n, bgr, bgr_stride, markers, marker_stride, rows, cols, depth, palette, dst,
+                         dst_stride);
+  }
+  if (probed) {
+    add_stats(c->stats, pst);
+    c->stats.batch_probe = 1;
+  }
+  c->stats.batch_mode = mode;
+  return rc;
+}
+
+// host_batch with the mode settled: 0 = run_batch (the full engine, `inflight` floods at a time),
+// 1 / 2 = the many-floods kernel.
+int host_batch_mode(msg_ctx* c, int mode, int n, const uint8_t* const* bgr, const size_t* bgr_stride,
+                    int32_t* const* markers, const size_t* marker_stride, const int* rows, const int* cols, int depth,
+                    const uint8_t* palette, uint8_t* const* dst, const size_t* dst_stride) {
+  if (!(mode && n > 0))
     return run_batch(c, n, [&](int k, msg_ctx* x) {
       return dst ? msg_watershed_colorize(x, bgr[k], bgr_stride[k], markers[k], marker_stride[k], rows[k], cols[k],
                                           depth, palette, dst[k], dst_stride[k], nullptr, 0)
@@ -1560,7 +1647,7 @@ int host_batch(msg_ctx* c, int n, const uint8_t* const* bgr, const size_t* bgr_s
                                (size_t)cols[k] * 4, rows[k], hipMemcpyHostToDevice, st));
   }
   HIPCHK(c, hipStreamSynchronize(st));  // the floods run on the sub-contexts' streams
-  int rc = batch_many(c, n, depth, dp,
+  int rc = batch_many(c, n, mode, depth, dp,
                       [&](int k, const uint8_t*& img, const int32_t*& mk, int& H, int& W, int32_t*& lab, uint8_t*& d) {
                         img = img_of(k);
                         mk = mk_of(k);
@@ -1634,26 +1721,64 @@ int msg_watershed_colorize_batch_dev(msg_ctx* c, int n, const void* const* d_bgr
   HIPCHK(c, hipSetDevice(c->dev));
   // the inputs may still be in flight on the caller's stream: the floods run on other streams
   HIPCHK(c, stream ? hipStreamSynchronize((hipStream_t)stream) : hipDeviceSynchronize());
-  if (c->many) {
-    for (int k = 0; k < n; ++k) {
-      if (rows[k] < 0 || cols[k] < 0) return fail(c, MSG_EINVAL, "negative size of frame %d", k);
-      if ((long long)rows[k] * cols[k] > 0 && (!d_bgr[k] || !d_markers_in[k] || !d_labels[k]))
-        return fail(c, MSG_EINVAL, "null device pointer of frame %d", k);
-    }
-    return batch_many(c, n, depth, (const uint8_t*)d_palette_bgr,
-                      [&](int k, const uint8_t*& img, const int32_t*& mk, int& H, int& W, int32_t*& lab, uint8_t*& dst) {
-                        img = (const uint8_t*)d_bgr[k];
-                        mk = (const int32_t*)d_markers_in[k];
-                        H = rows[k];
-                        W = cols[k];
-                        lab = (int32_t*)d_labels[k];
-                        dst = (uint8_t*)d_dst_bgr[k];
-                      });
+  for (int k = 0; k < n; ++k) {
+    if (rows[k] < 0 || cols[k] < 0) return fail(c, MSG_EINVAL, "negative size of frame %d", k);
+    if ((long long)rows[k] * cols[k] > 0 && (!d_bgr[k] || !d_markers_in[k] || !d_labels[k]))
+      return fail(c, MSG_EINVAL, "null device pointer of frame %d", k);
   }
-  return run_batch(c, n, [&](int k, msg_ctx* x) {
-    return msg_watershed_colorize_dev(x, d_bgr[k], d_markers_in[k], d_labels[k], rows[k], cols[k],
-                                      depth, d_palette_bgr, d_dst_bgr[k], nullptr, nullptr);
-  });
+  int mode = c->many, first = 0;
+  msg_stats pst{};
+  if (mode == 3) {  // automatic (auto_choice): the frame size's known choice, or a probe on frame 0
+    mode = 0;
+    const long long key = n > 0 ? ((long long)rows[0] << 32 | (unsigned)cols[0]) : -1;
+    if (n >= 2 && key == c->auto_key) {
+      mode = c->auto_mode;
+    } else if (n >= 2) {
+      const auto t0 = std::chrono::steady_clock::now();
+      int rc = msg_watershed_colorize_dev(c, d_bgr[0], d_markers_in[0], d_labels[0], rows[0], cols[0], depth,
+                                          d_palette_bgr, d_dst_bgr[0], nullptr, nullptr);
+      if (!rc && hipStreamSynchronize(c->own) != hipSuccess) rc = fail(c, MSG_EHIP, "probe flood stream failed");
+      if (rc) return rc;
+      const double ps = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      pst = c->stats;
+      first = 1;
+      mode = auto_choice(c, n - 1, pst, ps);
+      c->auto_key = key;
+      c->auto_mode = mode;
+    }
+  }
+  auto run_mode = [&](int m) {
+    const int nr = n - first;
+    if (m)
+      return batch_many(c, nr, m, depth, (const uint8_t*)d_palette_bgr,
+                        [&](int k, const uint8_t*& img, const int32_t*& mk, int& H, int& W, int32_t*& lab, uint8_t*& dst) {
+                          k += first;
+                          img = (const uint8_t*)d_bgr[k];
+                          mk = (const int32_t*)d_markers_in[k];
+                          H = rows[k];
+                          W = cols[k];
+                          lab = (int32_t*)d_labels[k];
+                          dst = (uint8_t*)d_dst_bgr[k];
+                        });
+    return run_batch(c, nr, [&](int k, msg_ctx* x) {
+      k += first;
+      return msg_watershed_colorize_dev(x, d_bgr[k], d_markers_in[k], d_labels[k], rows[k], cols[k],
+                                        depth, d_palette_bgr, d_dst_bgr[k], nullptr, nullptr);
+    });
+  };
+  int rc = run_mode(mode);
+  if (rc == MSG_ENOMEM && c->many == 3 && mode != 0) {  // automatic choice without the memory: the full engine
+    release_many(c);
+    (void)hipGetLastError();
+    c->auto_mode = mode = 0;
+    rc = run_mode(0);
+  }
+  if (first) {
+    add_stats(c->stats, pst);
+    c->stats.batch_probe = 1;
+  }
+  c->stats.batch_mode = mode;
+  return rc;
 }
 
 int msg_set_batch_devices(msg_ctx* c, int ndev, const int* devices) {
@@ -1679,7 +1804,7 @@ int msg_set_batch_devices(msg_ctx* c, int ndev, const int* devices) {
 }
 
 int msg_set_batch_floods(msg_ctx* c, int mode) {
-  if (!c || mode < 0 || mode > 2) return MSG_EINVAL;
+  if (!c || mode < 0 || mode > 3) return MSG_EINVAL;
   for (msg_ctx* sub : c->dsubs)
     if (sub) {
       const int rc = msg_set_batch_floods(sub, mode);
@@ -1687,14 +1812,11 @@ int msg_set_batch_floods(msg_ctx* c, int mode) {
     }
   (void)hipSetDevice(c->dev);
   c->many = mode;
+  c->auto_key = -1;  // mode 3 probes again
+  c->auto_mode = -1;
   if (mode == 0) {  // the mode's per-frame workspaces (~44 B/px each) are released with it
     if (hipSetDevice(c->dev) != hipSuccess) return fail(c, MSG_EHIP, "hipSetDevice failed");
-    for (msg_ctx* sub : c->msubs) msg_destroy(sub);
-    c->msubs.clear();
-    dfree(c->d_wss);
-    c->wss_cap = 0;
-    dfree(c->d_mstage);
-    c->mstage_cap = 0;
+    release_many(c);
   }
   return MSG_OK;
 }

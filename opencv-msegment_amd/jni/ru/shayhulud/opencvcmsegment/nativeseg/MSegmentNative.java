@@ -44,7 +44,7 @@ public final class MSegmentNative {
         long fresh = open(device);
         long old = CTX.get();
         CTX.set(fresh);
-        BATCH_MODE.get()[0] = 0;
+        BATCH_MODE.get()[0] = BATCH_AUTO;  // a fresh context starts in the library's default mode
         BATCH_DEVICES.set(new int[0]);
         defaultDevice = device;
         destroy(old);
@@ -184,27 +184,34 @@ public final class MSegmentNative {
         return markers;
     }
 
-    /** msg_set_batch_floods: 0 the full engine per flood, 1 / 2 many floods per launch. */
+    /** msg_set_batch_floods: 0 the full engine per flood, 1 / 2 many floods per launch, 3 automatic. */
     private static native int setBatchFloods(long ctx, int mode);
+
+    /** Batch modes of msg_set_batch_floods (msegment.h). */
+    public static final int BATCH_FULL_ENGINE = 0;
+    public static final int BATCH_MANY_FLOODS = 1;
+    public static final int BATCH_AUTO = 3;
 
     /** Returns 0 or a negative MSG_E* code; every markers[k] rewritten in place, every dsts[k] filled. */
     private static native int watershedColorizeBatch(long ctx, byte[][] bgrs, int[][] markers, int[] rows,
                                                      int[] cols, int depth, byte[] paletteOrNull, byte[][] dsts);
 
-    private static final ThreadLocal<int[]> BATCH_MODE = ThreadLocal.withInitial(() -> new int[]{0});
+    private static final ThreadLocal<int[]> BATCH_MODE = ThreadLocal.withInitial(() -> new int[]{BATCH_AUTO});
 
     /**
      * PictureService.watershed over many frames in one native call: the reference's evaluation
      * loop floods 92 frames per image (CorrelationTestService.java:84-86, 116, 128, 141, each through
      * PictureService.watershed at :852).  manyFloods = true selects msg_set_batch_floods mode 1
      * (every flood popped serially to its end, one wave per flood, all in one kernel: the mode for
-     * notConnectedMarkers' scattered seeds); false, the full engine per flood.  Labels are written
+     * notConnectedMarkers' scattered seeds); false, the library's automatic mode 3 (a probe flood per
+     * frame size picks the full engine or the many-floods kernel).  Labels are written
      * back into each markers Mat, and the colourised frames are returned in order.  One palette
      * (or null: colored = false) serves every frame, as one generateBGRColor draw per call would.
      */
     public static java.util.List<Mat> watershedBatch(java.util.List<Mat> srcs, java.util.List<Mat> markers,
                                                      int depth, byte[] paletteOrNull, boolean manyFloods) {
-        return watershedBatch(srcs, markers, depth, paletteOrNull, manyFloods, new int[0]);
+        return watershedBatch(srcs, markers, depth, paletteOrNull, manyFloods ? BATCH_MANY_FLOODS : BATCH_AUTO,
+                new int[0]);
     }
 
     /**
@@ -214,7 +221,7 @@ public final class MSegmentNative {
      * {0..7}: GPU r floods frames 8r..8r+7.
      */
     public static java.util.List<Mat> watershedBatch(java.util.List<Mat> srcs, java.util.List<Mat> markers,
-                                                     int depth, byte[] paletteOrNull, boolean manyFloods,
+                                                     int depth, byte[] paletteOrNull, int batchMode,
                                                      int[] devices) {
         int n = srcs.size();
         if (devices == null) {
@@ -244,9 +251,10 @@ public final class MSegmentNative {
             mk.get(0, 0, lab[k]);
         }
         long ctx = CTX.get();
-        int mode = manyFloods ? 1 : 0;
+        int mode = batchMode;
         int[] cur = BATCH_MODE.get();
         if (cur[0] != mode) {  // switching back to 0 releases the mode's per-frame workspaces
+            // switching to 0 releases the many-floods workspaces; 3 (automatic) keeps them for reuse
             int rc = setBatchFloods(ctx, mode);
             if (rc != 0) {
                 throw new CvException("libmsegment error " + rc + ": " + lastError(ctx));

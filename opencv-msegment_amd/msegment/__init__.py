@@ -239,7 +239,8 @@ class Segmenter:
 
     def set_batch_floods(self, mode=1):
         """Many floods per launch in the batch calls (msegment.h msg_set_batch_floods): 0 off, 1 every
-        flood serial to its end in one kernel (one wave per flood), 2 plateaus handed to batches."""
+        flood serial to its end in one kernel (one wave per flood), 2 plateaus handed to batches, 3
+        automatic (the library's default: a probe flood per frame size picks 0 or 1)."""
         self._check(self._L.msg_set_batch_floods(self._h, int(mode)))
 
     def set_resolve_grid(self, blocks=0):

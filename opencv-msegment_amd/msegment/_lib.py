@@ -68,7 +68,8 @@ class Stats(ctypes.Structure):
                 ("fast_pops", ctypes.c_int64), ("fast_pushes", ctypes.c_int64),
                 ("scatter_pops", ctypes.c_int64), ("scatter_pushes", ctypes.c_int64),
                 ("resolve_items", ctypes.c_int64), ("spec_exec_pops", ctypes.c_int64),
-                ("spec_longest_pops", ctypes.c_int64)]
+                ("spec_longest_pops", ctypes.c_int64), ("batch_mode", ctypes.c_int64),
+                ("batch_probe", ctypes.c_int64)]
 
 
 class KernelProfile(ctypes.Structure):

@@ -39,7 +39,7 @@ def frames():
     return out
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 def test_batch_many_host_buffers(seg, mode):
     fr = frames()
     work = [m.copy() for _, m in fr]
@@ -47,12 +47,13 @@ def test_batch_many_host_buffers(seg, mode):
     try:
         seg.watershed_batch([(img, w) for (img, _), w in zip(fr, work)])
     finally:
-        seg.set_batch_floods(0)
+        seg.set_batch_floods(0)  # releases the workspaces; back to the default (automatic) mode
+        seg.set_batch_floods(3)
     for k, ((img, m), got) in enumerate(zip(fr, work)):
         assert np.array_equal(got, ws_oracle.watershed(img, m)), k
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 def test_batch_many_device(seg, mode):
     import torch
 
@@ -67,7 +68,8 @@ def test_batch_many_device(seg, mode):
     try:
         seg.watershed_colorize_batch_dev(imgs, mks, labs, depth, None, dsts)
     finally:
-        seg.set_batch_floods(0)
+        seg.set_batch_floods(0)  # releases the workspaces; back to the default (automatic) mode
+        seg.set_batch_floods(3)
     torch.cuda.synchronize()
     for k, (img, m) in enumerate(fr):
         want = ws_oracle.watershed(img, m)
@@ -87,4 +89,45 @@ def test_batch_many_repeat_and_grow(seg):
             for k in range(n):
                 assert np.array_equal(work[k], ws_oracle.watershed(*fr[k])), (n, k)
     finally:
-        seg.set_batch_floods(0)
+        seg.set_batch_floods(0)  # releases the workspaces; back to the default (automatic) mode
+        seg.set_batch_floods(3)
+
+
+def test_auto_mode_probe_and_choice(seg):
+    """msg_set_batch_floods 3 (the default): the first call of a frame size floods frame 0 alone
+    (batch_probe) and picks the path; the next call of that size reuses the choice without a probe.
+    Plateau mosaics price far below a serial pop per pixel and stay on the full engine (mode 0);
+    scattered seeds on a textured frame (notConnectedMarkers' kind) take whichever path the probe
+    prices lower -- every frame bit-exact either way, host and device entry points."""
+    import torch
+
+    dev = torch.device("cuda", seg.device)
+    seg.set_batch_floods(3)
+    mos = [synth.frame("mosaic", 512, 512, 40 + k)[:2] for k in range(6)]
+    for call in range(2):
+        work = [m.copy() for _, m in mos]
+        seg.watershed_batch([(img, w) for (img, _), w in zip(mos, work)])
+        st = seg.stats()
+        assert st["batch_mode"] == 0 and st["batch_probe"] == (1 if call == 0 else 0), (call, st["batch_mode"])
+        for (img, m), got in zip(mos, work):
+            assert np.array_equal(got, ws_oracle.watershed(img, m))
+    rng = np.random.default_rng(5)
+    scat = []
+    for k in range(12):
+        img = synth.frame("mosaic_noise", 256, 256, 60 + k)[0]
+        m = np.where(rng.random((256, 256)) < 0.02, rng.integers(1, 6, (256, 256)), 0).astype(np.int32)
+        scat.append((img, m))
+    imgs = [torch.from_numpy(img).to(dev) for img, _ in scat]
+    mks = [torch.from_numpy(m).to(dev) for _, m in scat]
+    labs = [torch.empty_like(x) for x in mks]
+    dsts = [torch.empty(img.shape, dtype=torch.uint8, device=dev) for img, _ in scat]
+    for call in range(2):
+        seg.watershed_colorize_batch_dev(imgs, mks, labs, 5, None, dsts)
+        torch.cuda.synchronize()
+        st = seg.stats()
+        assert st["batch_mode"] in (0, 1) and st["batch_probe"] == (1 if call == 0 else 0)
+        for k, (img, m) in enumerate(scat):
+            assert np.array_equal(labs[k].cpu().numpy(), ws_oracle.watershed(img, m)), (call, k)
+    print("scattered seeds 256^2 x 12: automatic mode chose", st["batch_mode"])
+    seg.set_batch_floods(0)
+    seg.set_batch_floods(3)
