@@ -885,7 +885,7 @@ int batch_many(msg_ctx* c, int n, int mode, int depth, const uint8_t* d_pal, F f
   for (int k = 0; k < n && !rc; ++k)
     if (frs[k].N > 0 && hipStreamWaitEvent(c->own, ev[k], 0) != hipSuccess) rc = fail(c, MSG_EHIP, "stream wait failed");
   if (!rc) {
-    LAUNCH(c, KID_SERIAL_MULTI, c->own, k_serial_multi, dim3(n), dim3(SERIAL_MULTI_BS), 0, c->d_wss, n, run_limit);
+    LAUNCH(c, KID_SERIAL_MULTI, c->own, k_serial_multi, dim3(n), dim3(64), 0, c->d_wss, n, run_limit);
     if (hipGetLastError() != hipSuccess || hipEventRecord(ev[n], c->own) != hipSuccess)
       rc = fail(c, MSG_EHIP, "k_serial_multi launch failed");
   }

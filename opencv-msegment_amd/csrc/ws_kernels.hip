@@ -2782,116 +2782,37 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
 // pixels has no workspace (ctl == nullptr: flood_begin returns before binding it) and no work.
 // (Round 4 measured a form with deferred stores and LDS rings, k_serial's: album.jpg 1362 against
 // 1176 ms for this in-loop form; it was removed in round 5.)
-// Cache warming for the serial pops (round 6).  A serial pop's one dependent round trip -- the
-// popped pixel's neighbour states and weights, ~1 100 cycles when the lines come from MALL/HBM
-//  -- is most of its time.  While wave 0 pops, SERIAL_PF_WAVES more waves of the
-// block load the next queue entries of the lowest non-empty bucket and those items' neighbour
-// states and weights (SERIAL_PF_ITEMS ahead of the head), so that the lines are in the XCD's L2
-// when wave 0 pops them.  Loads only: the values are discarded (kept alive by an LDS store that
-// is never taken), the queue state is read racily as a hint, and nothing the serial wave reads or
-// writes changes -- results are identical with or without it.  The helpers leave once wave 0
-// raises `done`, which it does on every path out of its loop.
-#ifndef MSEG_SERIAL_PF_WAVES
-#define MSEG_SERIAL_PF_WAVES 2
-#endif
-constexpr int SERIAL_PF_WAVES = MSEG_SERIAL_PF_WAVES;
-constexpr int SERIAL_PF_PASS = 4;  // 64-item rounds per helper wave and pass
-constexpr int SERIAL_PF_ITEMS = (SERIAL_PF_WAVES > 0 ? SERIAL_PF_WAVES : 1) * SERIAL_PF_PASS * 64;
-constexpr int SERIAL_MULTI_BS = 64 * (1 + SERIAL_PF_WAVES);
-
-__device__ __forceinline__ void serial_prefetch(const Ws& ws, const int* s_qbase, const int* s_head, const int* s_tail,
-                                                const int* go, const int* done, int* sink, int hw) {
-  const int lane = lane_id();
-  const int Wt = ws.Wt, marg = ws.marg;
-  const int32_t* const mkb = ws.mk - marg;
-  const volatile int* const vh = s_head;
-  const volatile int* const vt = s_tail;
-  int last_lo = -1, last_h = 0;
-  unsigned acc = 0;
-  while (!*(const volatile int*)done) {
-    if (!*(const volatile int*)go) {
-      __builtin_amdgcn_s_sleep(4);
-      continue;
-    }
-    int lo = NQ;  // the lowest non-empty bucket, read racily (a hint)
-#pragma unroll
-    for (int k = 0; k < NQ / 64; ++k) {
-      const int l = lane * (NQ / 64) + k;
-      if (vt[l] > vh[l]) lo = min(lo, l);
-    }
-    lo = wave_min(lo);
-    if (lo >= NQ) {
-      __builtin_amdgcn_s_sleep(4);
-      continue;
-    }
-    const int h = vh[lo], t = vt[lo];
-    if (lo == last_lo && h < last_h + SERIAL_PF_ITEMS / 2) {  // the last pass is still ahead of the pops
-      __builtin_amdgcn_s_sleep(8);
-      continue;
-    }
-    const int qb = s_qbase[lo];
-#pragma unroll 1
-    for (int k = 0; k < SERIAL_PF_PASS; ++k) {
-      const int slot = h + (k * SERIAL_PF_WAVES + hw) * 64 + lane;
-      if (slot < t) {
-        const int p = ws.qbuf[qb + slot];
-        const int pb = p + marg;
-        unsigned v = (unsigned)ws.w4[p];
-#pragma unroll
-        for (int d = 0; d < 4; ++d) v ^= (unsigned)mkb[(unsigned)nbi(pb, d, Wt)];
-        acc += v;
-      }
-    }
-    last_lo = lo;
-    last_h = h;
-  }
-  if (acc == 0x9e3779b9u && lane == 0) *sink = (int)acc;  // keeps the loads; practically never taken
-}
-
-__global__ __launch_bounds__(SERIAL_MULTI_BS) void k_serial_multi(const Ws* __restrict__ wss, int n, int run_limit) {
+__global__ __launch_bounds__(64) void k_serial_multi(const Ws* __restrict__ wss, int n, int run_limit) {
   const int f = blockIdx.x;
   if (f >= n) return;
   const Ws ws = wss[f];
   Ctl* ctl = ws.ctl;
   if (ctl == nullptr || ws.N == 0) return;
-  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  const int lane = lane_id();
   const Batch B0 = ctl->bat;
-  if (ctl->done || ctl->error || B0.n == 0 || B0.mode != 0) return;  // (block-uniform)
+  if (ctl->done || ctl->error || B0.n == 0 || B0.mode != 0) return;
   __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ];
   __shared__ Seg s_seg[NQ];
   __shared__ Batch s_B;
   __shared__ int s_wcap, s_err, s_nseg, s_n, s_ser;
-  __shared__ int s_pfgo, s_pfdone, s_pfsink;
-  if (wv == 0) {
 #pragma unroll
-    for (int k = 0; k < NQ / 64; ++k) {
-      const int b = 64 * k + lane;
-      s_qbase[b] = ctl->qbase[b];
-      s_head[b] = ctl->qhead[b];
-      s_tail[b] = ctl->qtail[b];
-    }
-    if (lane == 0) {
-      s_B = B0;
-      s_B.mode = 0;
-      s_wcap = 0;
-      s_err = 0;
-      s_ser = 1;
-      s_pfgo = 1;
-      s_pfdone = 0;
-    }
+  for (int k = 0; k < NQ / 64; ++k) {
+    const int b = 64 * k + lane;
+    s_qbase[b] = ctl->qbase[b];
+    s_head[b] = ctl->qhead[b];
+    s_tail[b] = ctl->qtail[b];
   }
-  if (SERIAL_PF_WAVES > 0) {
-    __syncthreads();
-    if (wv > 0) {  // the helpers: warm the caches until wave 0 is done (no other exit)
-      serial_prefetch(ws, s_qbase, s_head, s_tail, &s_pfgo, &s_pfdone, &s_pfsink, wv - 1);
-      return;
-    }
+  if (lane == 0) {
+    s_B = B0;
+    s_B.mode = 0;
+    s_wcap = 0;
+    s_err = 0;
+    s_ser = 1;
   }
   wave_sync();
   long long cnt[4] = {0, 0, 0, 0};
   serial_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, cnt, 0, nullptr,
               run_limit);
-  if (lane == 0) *(volatile int*)&s_pfdone = 1;  // the helpers leave
   wave_sync();
   for (int k = lane; k < NQ; k += 64) {
     ctl->qhead[k] = s_head[k];
