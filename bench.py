@@ -149,15 +149,28 @@ def dist_env():
 
 
 def timed_steps(step, steps, barrier, sync):
-    """Barrier + sync on both sides of exactly `steps` steps; returns this rank's seconds."""
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    sync()
-    barrier()
-    return time.perf_counter() - t0
+    """Barrier + sync on both sides of exactly `steps` steps; returns this rank's seconds.  Python's
+    cyclic garbage collector is run before and paused inside the timed region: harness time, not the
+    library's.  (Round 6: this file's timed steps took 3.7-4.9 ms per headline frame on boxes where a
+    bare loop of the same call took 3.15-3.20 and the kernel trace showed every flood at ~3.2 ms --
+    a one-off stall of ~15 ms inside the timed region; profiles/r06e_headline_spread.txt.)"""
+    import gc
+
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        sync()
+        barrier()
+        return time.perf_counter() - t0
+    finally:
+        if was:
+            gc.enable()
 
 
 def reduce_max(x, device=None):
@@ -989,10 +1002,11 @@ def main(argv=None):
     elif SHAPE or COLOR:
         pipe_key = "%s_%s_%dx%d_s%d" % (args.pipeline, args.kind, S, S, seed)
 
-    for _ in range(args.warmup):
-        step()
+    # one step for the parity check, then the warm-up steps right before the timed ones (the check's
+    # host work -- a 64 MB read-back and its hash -- used to sit between warm-up and timing, leaving
+    # the GPU idle for ~80 ms just before the first timed step)
+    step()
     sync()
-    st = seg.stats()
     parity = None
     dgs = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
     dkey = "%s_%dx%d_s%d" % (args.kind, S, S, seed)
@@ -1018,6 +1032,10 @@ def main(argv=None):
         if rank == 0:
             log("[rank 0] parity:", parity)
 
+    for _ in range(args.warmup):
+        step()
+    sync()
+    st = seg.stats()
     dt = timed_steps(step, args.steps, barrier, sync)
     dt_max = reduce_max(dt, cdev)
     value = whole_job_mpx(world, K * S * S, args.steps, dt_max)
