@@ -713,14 +713,19 @@ constexpr int MAX_INFLIGHT = 8;
 // diag is zeroed: a frame's diag is one of several banks (k_resolve cycles with a max-type slot, or
 // the speculative round split), chosen per frame, so sums over frames would mix units and add
 // maxima (msegment.h: diag is reported for single floods only).
+// batch_mode / batch_probe are flags, not counts: the largest over the parts (e.g. the devices of a
+// msg_set_batch_devices call).
 void add_stats(msg_stats& tot, const msg_stats& s) {
   static_assert(sizeof(msg_stats) % sizeof(int64_t) == 0, "msg_stats is int64 fields only");
+  const int64_t mode = std::max(tot.batch_mode, s.batch_mode), probe = std::max(tot.batch_probe, s.batch_probe);
   int64_t* t = reinterpret_cast<int64_t*>(&tot);
   const int64_t* a = reinterpret_cast<const int64_t*>(&s);
   for (size_t k = 0; k < sizeof(msg_stats) / sizeof(int64_t); ++k) t[k] += a[k];
   tot.rows = s.rows;
   tot.cols = s.cols;
   for (auto& d : tot.diag) d = 0;
+  tot.batch_mode = mode;
+  tot.batch_probe = probe;
 }
 
 int ensure_subs(msg_ctx* c, int k) {

@@ -153,3 +153,24 @@ def test_bench_rejects_gpus_world_mismatch():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
                          capture_output=True, text=True, timeout=120)
     assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_config5_on_one_gpu():
+    """bench.py's N = 2 path end to end on the GPU box's one GPU (MSEG_BENCH_SHARED_GPU: both ranks on
+    GPU 0, gloo for the timing and parity collectives): each rank floods its 8 config-5 frames as one
+    batch call, checks them against the oracle digests, and rank 0 prints the summed count."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, MSEG_BENCH_SHARED_GPU="1")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                          "--no-profile-pass"], env=env, capture_output=True, text=True, timeout=280)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["config"]["frames_per_rank_per_step"] == 8
+    assert d["parity"].startswith("16/16 frames bit-exact"), d["parity"]
+    assert "rehearsal" in d["config"]
