@@ -72,6 +72,7 @@ struct msg_ctx {
   // host-mapped progress mirror {iteration, done, error, remaining}, written by k_scatter
   int* h_mir = nullptr;
   int* d_mir = nullptr;  // its device address
+  Ctl* h_tail = nullptr;  // pinned copy of the control block read back at the end of a flood
   // ordering with the legacy null stream for device calls given stream = NULL (StreamScope)
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   unsigned epoch = 1;
@@ -530,7 +531,11 @@ int flood_loop(msg_ctx* c, FloodRun& fr) {
   __atomic_store_n(&c->h_mir[0], -1, __ATOMIC_RELEASE);
   c->h_mir[4] = 0;
   c->h_mir[5] = 0;
-  c->h_mir[6] = 0;
+  // the first two groups are queued before any report: assume a large flood batch (two-launch
+  // iterations), as phase 1's queue usually is -- a wrong guess costs a declined commit or a small
+  // batch committed by the grid instead of k_scan's loop, never a wrong result (every kernel checks
+  // the batch it serves).  The three-launch start cost the headline frame ~8 x 4 us (r05p trace).
+  c->h_mir[6] = 1;
   int it = 0, prev_end = -1;
   c->group = 4;
   long long syncs = 0;
@@ -616,11 +621,12 @@ int flood_end(msg_ctx* c, FloodRun& fr, int32_t* d_labels, int depth = 0, const 
            depth, d_pal, d_dst, d_gray, &c->d_ctl->error);
     HIPCHK(c, hipGetLastError());
   }
-  Ctl tail;
-  HIPCHK(c, hipMemcpyAsync(&tail, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
+  // into pinned memory: a copy to pageable memory is staged and synchronous on its own
+  HIPCHK(c, hipMemcpyAsync(c->h_tail, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
   unsigned long long dgv[32] = {0};
   if (c->diag) HIPCHK(c, hipMemcpyAsync(dgv, c->d_diag, sizeof(dgv), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
+  const Ctl& tail = *c->h_tail;
   c->stats.host_syncs += 1;
   if (c->prof) collect_profile(c);
   c->stats.batches = tail.batches;
@@ -1119,6 +1125,7 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
       hipHostMalloc((void**)&c->h_mir, 8 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer((void**)&c->d_mir, c->h_mir, 0) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_tail, sizeof(Ctl), hipHostMallocDefault) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming) != hipSuccess) {
     msg_destroy(c);
@@ -1186,6 +1193,7 @@ void msg_destroy(msg_ctx* c) {
   dfree(c->d_cmcnt);
   if (c->h_hist) (void)hipHostFree(c->h_hist);
   if (c->h_mir) (void)hipHostFree(c->h_mir);
+  if (c->h_tail) (void)hipHostFree(c->h_tail);
   for (auto& e : c->evpool) (void)hipEventDestroy(e);
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
   if (c->ev_out) (void)hipEventDestroy(c->ev_out);

@@ -8,7 +8,7 @@ OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 for rep in 1 2; do
   for lib in "$@"; do
     name=$(basename "$lib" .so)
-    MSEGMENT_LIB=$(realpath "$lib") timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-profile-pass --stress-steps 0 --batch-frames 1 --many-frames 0 \
+    MSEGMENT_LIB=$(realpath "$lib") timeout -k 10 300 python bench.py ${AB_ARGS:-} --steps 20 --warmup 3 --no-cpu-baseline --no-profile-pass --stress-steps 0 --batch-frames 1 --many-frames 0 --correlation= \
       > "$OUT/$name.$rep.log" 2>&1
     rc=$?
     [ $rc -eq 0 ] || { echo "STOP $name rc=$rc"; exit $rc; }
