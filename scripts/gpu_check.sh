@@ -25,7 +25,7 @@ if [ -z "${PROF_ONLY:-}" ]; then
 fi
 # the profiled command is the headline's single-flood path only (--batch-frames 1: no concurrent
 # floods, whose overlapping kernels would inflate the per-launch durations and traffic)
-PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass --batch-frames 1 --stress-steps 0 --no-hwq4 --many-frames 0"
+PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass --batch-frames 1 --stress-steps 0 --no-hwq4 --many-frames 0 --correlation="
 run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py $PROF_ARGS
 find "$OUT/prof" -name '*stats*' -exec cp {} "$OUT/" \; 2>/dev/null
 # HBM traffic: one counter group per rocprofv3 run, kernel trace only (MI355X_MICROARCH.md)
@@ -38,7 +38,7 @@ python scripts/pmc_summary.py "$OUT" "$OUT/pmc_latest.json" "$TAG, libmsegment b
 # the config-3 stress variants (speculative engine, serial pops): kernel stats and HBM traffic
 if [ -n "${STRESS_PROF:-}" ]; then
   for kind in mosaic_noise random; do
-    SARGS="--kind $kind --steps 1 --warmup 1 --no-cpu-baseline --no-profile-pass --batch-frames 0 --stress-steps 0 --no-hwq4 --many-frames 0"
+    SARGS="--kind $kind --steps 1 --warmup 1 --no-cpu-baseline --no-profile-pass --batch-frames 0 --stress-steps 0 --no-hwq4 --many-frames 0 --correlation="
     run rocprof_$kind 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$kind" -o run -- python bench.py $SARGS
     find "$OUT/prof_$kind" -name '*kernel_stats*' -exec cp {} "$OUT/${kind}_kernel_stats.csv" \; 2>/dev/null
     for ctr in FETCH_SIZE WRITE_SIZE; do
