@@ -533,20 +533,12 @@ def correlation_image(name):
     return synth.frame(name, 1024, 1024, 100)[0], "%s 1024x1024 seed 100" % name
 
 
-def correlation_line(seg, sync, dev, name, cpu=True, steps=2):
-    """The reference's real call pattern for the flood: CorrelationTestService floods ONE image 92
-    times per test -- 90 notConnectedMarkers marker maps (5 depths x 3 mask sizes x 6 option sets),
-    the shape method's and the colour method's (whose flood source is the sharpened image).  The
-    marker maps come from the GPU marker stages (outside the timed region); each step is ONE batch
-    call of the 92 floods + colorByIndexes in the many-floods mode (msg_set_batch_floods 1), the
-    default batch path (full engine per flood, 4 in flight) timed once beside it, and the C oracle
-    over the same 92 floods on the host's threads, whose labels are the parity check."""
-    import numpy as np
+def correlation_markers(seg, dev, t_img):
+    """CorrelationTestService.test's 92 marker maps of one image (device tensor t_img) from the GPU
+    marker stages: (flood sources, markers, depths, names, the colour method's sharpened image)."""
     import torch
 
-    img, desc = correlation_image(name)
-    H, W = img.shape[:2]
-    t_img = torch.from_numpy(img).to(dev)
+    H, W = t_img.shape[:2]
     srcs, mks, depths, names = [], [], [], []
     for depth in CORR_DEPTHS:
         for mask in CORR_MASKS:
@@ -570,6 +562,94 @@ def correlation_line(seg, sync, dev, name, cpu=True, steps=2):
     srcs.append(t_sharp)
     mks.append(m)
     names.append("COLOR")
+    return srcs, mks, depths, names, t_sharp
+
+
+def correlation_mass_line(seg, sync, dev, images=8, S=1024, cpu=True, steps=2):
+    """CorrelationTestService.massTest (CorrelationTestService.java:49-53) runs test() over a map of
+    images: batched at that level, the 92 floods of each of `images` images (1024^2 noisy mosaics,
+    seeds 100..) go to ONE call -- the many-floods kernel then has 92 x images floods in flight.
+    Every flood checked against the C oracle; the 16-thread oracle over the same floods beside it."""
+    import numpy as np
+    import torch
+
+    from msegment import synth
+
+    srcs, mks, depths, keep = [], [], [], []
+    for k in range(images):
+        t_img = torch.from_numpy(synth.frame("mosaic_noise", S, S, 100 + k)[0]).to(dev)
+        s_k, m_k, d_k, _, t_sharp = correlation_markers(seg, dev, t_img)
+        srcs += s_k
+        mks += m_k
+        depths += d_k
+        keep += [t_img, t_sharp]
+    sync()
+    n = len(mks)
+    depth = max(depths)
+    labs = [torch.empty_like(x) for x in mks]
+    dsts = [torch.empty((S, S, 3), dtype=torch.uint8, device=dev) for _ in mks]
+    seg.set_batch_floods(1)
+    try:
+        seg.watershed_colorize_batch_dev(srcs, mks, labs, depth, None, dsts)  # warm-up (workspaces)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            seg.watershed_colorize_batch_dev(srcs, mks, labs, depth, None, dsts)
+        sync()
+        dt = time.perf_counter() - t0
+    finally:
+        seg.set_batch_floods(0)
+        seg.set_batch_floods(3)
+    out = {"workload": "CorrelationTestService.massTest batched: %d images (mosaic_noise %dx%d seeds 100..%d) x 92 "
+                       "floods (90 notConnectedMarkers marker maps, the shape and the colour method's) = %d floods "
+                       "+ colorByIndexes in ONE batch call, device-resident, many-floods mode"
+                       % (images, S, S, 99 + images, n),
+           "value": round(n * S * S * steps / dt / 1e6, 3), "unit": "Mpx/s", "floods": n, "steps": steps,
+           "ms_per_step": round(1000.0 * dt / steps, 3)}
+    if cpu:
+        from concurrent.futures import ThreadPoolExecutor
+
+        from oracle import ws_oracle
+
+        nt = batch_cpu_threads(n)
+        src_host = {id(x): x.cpu().numpy() for x in keep}
+        m_host = [x.cpu().numpy() for x in mks]
+
+        def one(k):
+            lab = ws_oracle.watershed(src_host[id(srcs[k])], m_host[k])
+            ws_oracle.colorize(lab, depth, None)
+            return lab
+
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(nt) as ex:
+            want = list(ex.map(one, range(n)))
+        cdt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(n * S * S / cdt / 1e6, 3), "unit": "Mpx/s", "cores": nt, "kind": "port",
+                               "sample": "the same %d floods (the GPU's marker maps), one flood per thread: "
+                                         "oracle/ws_oracle.c watershed + colorize, %.2f s" % (n, cdt)}
+        bad = sum(not np.array_equal(labs[k].cpu().numpy(), want[k]) for k in range(n))
+        out["parity"] = "%d/%d floods bit-exact vs the C oracle" % (n - bad, n)
+        del want, m_host
+    del srcs, mks, labs, dsts, keep
+    torch.cuda.empty_cache()
+    return out
+
+
+def correlation_line(seg, sync, dev, name, cpu=True, steps=2):
+    """The reference's real call pattern for the flood: CorrelationTestService floods ONE image 92
+    times per test -- 90 notConnectedMarkers marker maps (5 depths x 3 mask sizes x 6 option sets),
+    the shape method's and the colour method's (whose flood source is the sharpened image).  The
+    marker maps come from the GPU marker stages (outside the timed region); each step is ONE batch
+    call of the 92 floods + colorByIndexes in the many-floods mode (msg_set_batch_floods 1), the
+    default batch path (full engine per flood, 4 in flight) timed once beside it, and the C oracle
+    over the same 92 floods on the host's threads, whose labels are the parity check."""
+    import numpy as np
+    import torch
+
+    img, desc = correlation_image(name)
+    H, W = img.shape[:2]
+    t_img = torch.from_numpy(img).to(dev)
+    srcs, mks, depths, names, t_sharp = correlation_markers(seg, dev, t_img)
     sync()
     n = len(mks)
     depth = max(depths)
@@ -879,6 +959,8 @@ def main(argv=None):
     ap.add_argument("--correlation", default="mosaic_noise,album",
                     help="images of the correlation line (CorrelationTestService's 92 floods of one image "
                          "per call): comma list of mosaic_noise / random / mosaic (1024^2) / album; '' = skip")
+    ap.add_argument("--correlation-images", type=int, default=8,
+                    help="images of the correlation line's massTest object (92 floods each, one call); 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile-pass", action="store_true")
     ap.add_argument("--batch-only", action="store_true", help=argparse.SUPPRESS)
@@ -1075,6 +1157,9 @@ def main(argv=None):
         corr = {}
         for name in args.correlation.split(","):
             corr[name] = correlation_line(seg, sync, dev, name, cpu=not args.no_cpu_baseline)
+        if args.correlation_images > 0:
+            corr["mass"] = correlation_mass_line(seg, sync, dev, images=args.correlation_images,
+                                                 cpu=not args.no_cpu_baseline)
 
     stress = stress_random = None
     if rank == 0 and world == 1 and K == 1 and not MARKERS and args.kind == "mosaic" and args.stress_steps > 0:
