@@ -71,19 +71,12 @@ __device__ __forceinline__ void st_ag32(int* p, int v) {
 __device__ __forceinline__ void claim_max(unsigned long long* p, unsigned long long k) {
   __hip_atomic_fetch_max(p, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Wait for every vector memory operation of the wave (s_waitcnt vmcnt(0); expcnt and lgkmcnt left
-// alone).  A pop's loads are waited for explicitly BEFORE the previous pop's claims, label and
-// record are issued: the counter retires in issue order, and with those writes issued after the
-// loads in branches some lanes (or the whole wave) skip, the compiler's own wait at the first use
-// of a loaded value is vmcnt(0) behind the writes too -- their acknowledgements (atomics at the L2
-// or beyond) then sat on every pop's critical path.  Issued after the wait, the writes complete
-// while the pop is decided and the next pop's loads are in flight.
-// The immediate is the gfx9 encoding (vmcnt[3:0] = 0, expcnt and lgkmcnt at their maxima, vmcnt[5:4]
-// = 0); gfx10+ lay the fields out differently, so any other target is refused at compile time.
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
-#error "vm_drain: s_waitcnt 0x0F70 is vmcnt(0) only in the gfx9 encoding (build for gfx950)"
-#endif
-__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// vm_drain (ws_kernels.hip): a pop's loads are waited for explicitly BEFORE the previous pop's
+// claims, label and record are issued: the counter retires in issue order, and with those writes
+// issued after the loads in branches some lanes (or the whole wave) skip, the compiler's own wait at
+// the first use of a loaded value is vmcnt(0) behind the writes too -- their acknowledgements
+// (atomics at the L2 or beyond) then sat on every pop's critical path.  Issued after the wait, the
+// writes complete while the pop is decided and the next pop's loads are in flight.
 
 __device__ __forceinline__ unsigned long long fin_word(unsigned G, unsigned popped, int lab) {
   return ((unsigned long long)G << 33) | ((unsigned long long)popped << 32) | (uint32_t)lab;

@@ -2358,6 +2358,17 @@ __device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qba
 // or when the queue is empty, forming the next batch.
 
 
+// Wait for every vector memory operation of the wave (s_waitcnt vmcnt(0); expcnt and lgkmcnt left
+// alone), where the code knows a wait is due, so that the compiler need not place one where it
+// cannot tell (a register written by a load in a branch, read after the join: its own wait there
+// is vmcnt(0), behind every store issued since).
+// The immediate is the gfx9 encoding (vmcnt[3:0] = 0, expcnt and lgkmcnt at their maxima, vmcnt[5:4]
+// = 0); gfx10+ lay the fields out differently, so any other target is refused at compile time.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "vm_drain: s_waitcnt 0x0F70 is vmcnt(0) only in the gfx9 encoding (build for gfx950)"
+#endif
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 __device__ __forceinline__ int ld_state_v(const Ws& ws, int t) {
   return __hip_atomic_load(ws.mk + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -2405,6 +2416,9 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
       ring_h0 = h;
       ring_n = min(navail, 64);
       ring = (lane < ring_n) ? ld_qbuf_v(ws, s_qbase[lo] + h + lane) : 0;
+      // the ring is waited for here, once per refill: left to the compiler, the wait sits at the
+      // readlane below on EVERY pop, as vmcnt(0) behind the previous pop's label and queue stores
+      vm_drain();
     }
     const int p = __builtin_amdgcn_readlane(ring, h - ring_h0);  // a uniform lane: no LDS crossbar
     const int pb = p + marg;
@@ -2767,6 +2781,151 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
   }
 }
 
+// serial_loop_lanes: serial_loop's pops for a wave that has its flood to itself (k_serial_multi),
+// with the pop's memory work spread over lanes: lane d < 4 loads the state of neighbour d and the
+// other lanes the pixel's weights, in ONE load instruction; a pop's pushes are one store of queue
+// slots and one of states (the popped pixel's label in the same instruction, lanes >= 4), their
+// slots ranked among the pushing lanes in direction order (cv::watershed's push order).  The head
+// of the popped bucket stays in a register while the loop stays on it; its next 64 slots sit in
+// a register ring, so a pop only looks at the bucket's tail when the ring runs out.  Same pops,
+// same order, same states as serial_loop, whose pop is ~180 instructions of scalar address
+// arithmetic and an LDS round trip per push, issued one at a time by a lone wave (round 6: 92
+// notConnectedMarkers floods of one 1024^2 image 134 -> 170 Mpx/s, profiles/r06k_ab_serial_lanes.log).
+// Values the loop branches on are read from LDS through readfirstlane (and no store sits in a
+// lane-divergent branch of its own): otherwise the compiler keeps them in vector registers and
+// turns every branch of the loop into exec-mask code.
+__device__ void serial_loop_lanes(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qbase, int* s_head,
+                                  int* s_tail, int* s_wcap, int* s_err, int* s_nseg, int* s_n, int* s_ser,
+                                  long long* cnt, int run_limit) {
+  const int lane = lane_id();
+  const int marg = ws.marg;
+  const int row = ws.Wt << 4;
+  const Batch B0 = *s_B;
+  // lane d < 4: neighbour d of tiled pixel pb is pb + (((pb & msk) != val) ? dn : dw) (nbi)
+  const int d = lane & 3;
+  const int msk = (d < 2) ? 3 : 12;
+  const int val = (d == 0) ? 0 : (d == 1) ? 3 : (d == 2) ? 0 : 12;
+  const int dn = (d == 0) ? -1 : (d == 1) ? 1 : (d == 2) ? -4 : 4;
+  const int dw = (d == 0) ? -13 : (d == 1) ? 13 : (d == 2) ? 12 - row : row - 12;
+  const bool nbl = lane < 4;
+  const int* ldbase = nbl ? ws.mk : ws.w4;
+  const unsigned qcap32 = (unsigned)min(ws.qcap, (long long)0x7fffffff);
+  int pops = 0, pushes = 0, run = 0;
+  int lo = __builtin_amdgcn_readfirstlane(lowest_bucket(s_head, s_tail, 0));
+  int cl = -1, ch = 0, cb = 0;  // the bucket being popped: level, head (in a register), queue base
+  int ring = 0, ring_h0 = 0, ring_end = 0;
+  while (lo < NQ) {
+    if (lo != cl) {  // switch buckets (every lane stores the same value: no divergent branch)
+      if (cl >= 0) s_head[cl] = ch;
+      wave_sync();
+      cl = lo;
+      ch = __builtin_amdgcn_readfirstlane(s_head[lo]);
+      cb = __builtin_amdgcn_readfirstlane(s_qbase[lo]);
+      ring_end = ch;  // the ring is refilled before the first pop
+    }
+    if (ch >= ring_end) {  // the ring ran out: the bucket's tail decides
+      const int ct = __builtin_amdgcn_readfirstlane(s_tail[cl]);
+      if (ch >= ct) {  // empty: the next one up (LDS is current but for cl's head)
+        s_head[cl] = ch;
+        wave_sync();
+        cl = -1;
+        lo = __builtin_amdgcn_readfirstlane(lowest_bucket(s_head, s_tail, lo + 1));
+        continue;
+      }
+      ring_h0 = ch;  // its next 64 slots, one load per lane
+      ring_end = ch + min(ct - ch, 64);
+      ring = (ch + lane < ring_end) ? ld_qbuf_v(ws, cb + ch + lane) : 0;
+      vm_drain();
+    }
+    if (run >= run_limit) break;
+    if (ws.spec_lazy && pops >= 4096) break;
+    const int p = __builtin_amdgcn_readlane(ring, ch - ring_h0);
+    const int pb = p + marg;
+    const int idx = nbl ? pb + (((pb & msk) != val) ? dn : dw) - marg : p;
+    const int v = __hip_atomic_load(ldbase + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const unsigned w4 = (unsigned)__builtin_amdgcn_readlane(v, 4);
+    // the fold of the settled neighbours (fold_lab in direction order): 0 if none, their label if
+    // they agree, WSHED otherwise -- i.e. from their largest and smallest label
+    const bool pos = nbl && v > 0;
+    int mx = pos ? v : 0, mn = pos ? v : 0x7fffffff;
+    mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+    mn = min(mn, __builtin_amdgcn_update_dpp(0x7fffffff, mn, 0xB1, 0xF, 0xF, false));
+    mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+    mn = min(mn, __builtin_amdgcn_update_dpp(0x7fffffff, mn, 0x4E, 0xF, 0xF, false));
+    const int smx = __builtin_amdgcn_readfirstlane(mx), smn = __builtin_amdgcn_readfirstlane(mn);
+    int lab = (smx == 0) ? 0 : (smx == smn ? smx : WSHED);
+    const bool bad = lab == 0;  // impossible for an exact queue
+    if (bad) {
+      *s_err = ERR_STATE;
+      lab = WSHED;
+    }
+    ++ch;
+    ++pops;
+    // pushing lanes: neighbours in state 0 of a labelled pixel
+    const bool push = nbl && v == 0 && lab != WSHED;
+    const unsigned pm = (unsigned)__ballot(push);
+    int sv = lab;  // lanes >= 4: the popped pixel's label (idx == p)
+    int newlo = lo;
+    bool ok = !nbl;  // lanes that store a state
+    if (pm) {
+      const int t = (int)((w4 >> (8 * d)) & 255u);
+      const int qb = s_qbase[t], qt = s_tail[t];
+      int rank = 0;  // earlier pushing lanes of the same bucket (direction order)
+      if (pm & (pm - 1)) {
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+          rank += (((pm >> e) & 1u) && e < lane && (int)((w4 >> (8 * e)) & 255u) == t) ? 1 : 0;
+      }
+      const int dest = qb + qt + rank;
+      if (__ballot(push && (unsigned)dest >= qcap32)) {
+        *s_err = ERR_CAPACITY;
+        break;
+      }
+      atomicAdd(&s_tail[t], push ? 1 : 0);  // (adds commute; lanes of the same bucket each add 1)
+      pushes += __builtin_popcount(pm);
+      int tm = push ? t : NQ;
+      tm = min(tm, __builtin_amdgcn_update_dpp(NQ, tm, 0xB1, 0xF, 0xF, false));
+      tm = min(tm, __builtin_amdgcn_update_dpp(NQ, tm, 0x4E, 0xF, 0xF, false));
+      newlo = min(lo, __builtin_amdgcn_readfirstlane(tm));
+      sv = push ? queued_state(dest) : lab;
+      ok = ok || push;
+      if (push) ws.qbuf[dest] = idx;
+    }
+    // the popped pixel's label and the pushed neighbours' queue states: one store
+    if (ok) ws.mk[idx] = sv;
+    run = (newlo < lo) ? 0 : run + 1;
+    lo = newlo;
+    if (bad) break;
+  }
+  if (cl >= 0) s_head[cl] = ch;
+  wave_sync();
+  if (lane == 0) {
+    cnt[0] += pops;
+    cnt[1] += pops;
+    cnt[2] += pushes;
+    *s_wcap = 0;  // the next batch: a whole generation
+  }
+  wave_sync();
+  form_batch(s_qbase, s_head, s_tail, 0, 0, s_seg, s_nseg, s_n);
+  wave_sync();
+  if (lane == 0) {
+    Batch nb;
+    nb.mode = 0;
+    nb.epoch = B0.epoch + 1;
+    nb.ncommit = 0;
+    nb.nchunk = 0;
+    nb.rrun = 0;
+    nb.nseg = *s_nseg;
+    nb.n = (*s_nseg > 0) ? *s_n : 0;
+    nb.L = (*s_nseg > 0) ? s_seg[0].L : -1;
+    nb.bstart = (*s_nseg > 0) ? s_seg[0].bstart : 0;
+    *s_B = nb;
+    *s_ser = 0;
+    cnt[3] += pops;
+  }
+  wave_sync();
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_serial_multi: the serial pops of MANY floods in one launch (the batch entry points' many-floods
 // mode, msg_set_batch_floods): block f = one wave = flood f, each flood in its own workspace
@@ -2785,7 +2944,14 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
 __global__ __launch_bounds__(64) void k_serial_multi(const Ws* __restrict__ wss, int n, int run_limit) {
   const int f = blockIdx.x;
   if (f >= n) return;
-  const Ws ws = wss[f];
+  // loaded through the constant address space, the workspace's pointers are taken for global ones
+  // (global_load / global_store; flat ones also count against the LDS counter, so that every LDS
+  // wait of the pop loop also waited for the previous pop's stores)
+#if defined(__HIP_DEVICE_COMPILE__)
+  const Ws ws = ((const __attribute__((address_space(4))) Ws*)wss)[f];
+#else
+  const Ws ws = wss[f];  // the host pass of the single-source build: never runs
+#endif
   Ctl* ctl = ws.ctl;
   if (ctl == nullptr || ws.N == 0) return;
   const int lane = lane_id();
@@ -2811,8 +2977,8 @@ __global__ __launch_bounds__(64) void k_serial_multi(const Ws* __restrict__ wss,
   }
   wave_sync();
   long long cnt[4] = {0, 0, 0, 0};
-  serial_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, cnt, 0, nullptr,
-              run_limit);
+  serial_loop_lanes(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, cnt,
+                    run_limit);
   wave_sync();
   for (int k = lane; k < NQ; k += 64) {
     ctl->qhead[k] = s_head[k];
