@@ -2193,8 +2193,8 @@ __device__ __forceinline__ bool attempt_item_slots(const Item& it, const int (&v
 // wave_rank on the queue state the small loop keeps in LDS (in-order LDS within one wave).
 // Returns when the next batch has more than 64 items, the flood is done, or on error.
 constexpr int TINY_MAX = 64;
-constexpr int SERIAL_RUN = 4096;    // serial_loop: clean pops after which batches pay again
-constexpr int SERIAL_SWITCH = 16;   // a tiny batch cut before this many items -> serial_loop
+constexpr int SERIAL_RUN = 4096;    // serial pops: clean pops after which batches pay again
+constexpr int SERIAL_SWITCH = 16;   // a tiny batch cut before this many items -> serial pops
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -2346,17 +2346,12 @@ __device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qba
 }
 
 // Serial pops: cv::watershed's own phase-2 loop (pop the oldest item of the lowest non-empty
-// bucket, fold its labelled neighbours, push its unknown ones in L,R,T,B order), run by wave 0 on
-// the engine's own queue and state, for the interrupt-dense regime where batches commit a few
-// items each.  Every lane executes the same scalar program on the same addresses (uniform loads
-// and stores coalesce to one request each; vector atomics keep the loads off the scalar cache,
-// which does not see vector stores), so every lane's loads follow its own stores and no wait or
-// barrier is needed between pops; the lanes only share the work of prefetching the next 64 queue
-// slots of the popped bucket.  Entered when a tiny batch commits fewer than SERIAL_SWITCH items before an
-// interrupt (a pop costs ~0.55 us here against ~7 us per tiny batch: scripts/regime_probe.py);
-// returns once a run of SERIAL_RUN pops pushed nothing below the popped level (batches pay again),
-// or when the queue is empty, forming the next batch.
-
+// bucket, fold its labelled neighbours, push its unknown ones in L,R,T,B order) on the engine's own
+// queue and state, for the interrupt-dense regime where batches commit a few items each: run by
+// k_scan's wave 0 when a tiny batch commits fewer than SERIAL_SWITCH items before an interrupt, and
+// by k_serial_multi's waves on many floods at once (serial_loop_lanes below).  Returns once a run
+// of SERIAL_RUN pops pushed nothing below the popped level (batches pay again), or when the queue
+// is empty, forming the next batch.
 
 // Wait for every vector memory operation of the wave (s_waitcnt vmcnt(0); expcnt and lgkmcnt left
 // alone), where the code knows a wait is due, so that the compiler need not place one where it
@@ -2369,9 +2364,6 @@ __device__ void tiny_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qba
 #endif
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
-__device__ __forceinline__ int ld_state_v(const Ws& ws, int t) {
-  return __hip_atomic_load(ws.mk + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 __device__ __forceinline__ int ld_qbuf_v(const Ws& ws, int slot) {
   return __hip_atomic_load(ws.qbuf + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -2388,22 +2380,57 @@ __device__ __forceinline__ int lowest_bucket(const int* head, const int* tail, i
   return wave_min(lo);
 }
 
-__device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qbase, int* s_head, int* s_tail,
-                            int* s_wcap, int* s_err, int* s_nseg, int* s_n, int* s_ser, long long* cnt,
-                            int spec_block, int* spec_cool, int run_limit = SERIAL_RUN) {
+// serial_loop_lanes: the serial pops of one wave, with the pop's memory work spread over lanes:
+// lane d < 4 loads the state of neighbour d and the other lanes the pixel's weights, in ONE load
+// instruction; a pop's pushes are one store of queue slots and one of states (the popped pixel's
+// label in the same instruction, lanes >= 4), their slots ranked among the pushing lanes in
+// direction order (cv::watershed's push order).  The head of the popped bucket stays in a register
+// while the loop stays on it; its next 64 slots sit in a register ring, so a pop only looks at the
+// bucket's tail when the ring runs out.  Round 6 replaced a form whose every lane ran the same
+// scalar program (~180 instructions a pop of scalar address arithmetic and an LDS round trip per
+// push, issued one at a time by a lone wave): 92 notConnectedMarkers floods of one 1024^2 image
+// 134 -> 170 Mpx/s (profiles/r06k_ab_serial_lanes.log), one such flood in k_scan 900 -> 810 ms
+// (profiles/r06o_ab_serial_lanes_kscan.log).  The loads stay vector atomics: off the scalar cache,
+// which does not see vector stores.
+// Values the loop branches on are read from LDS through readfirstlane (and no store sits in a
+// lane-divergent branch of its own): otherwise the compiler keeps them in vector registers and
+// turns every branch of the loop into exec-mask code.
+template <bool RELANE>
+__device__ void serial_loop_lanes(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qbase, int* s_head,
+                                  int* s_tail, int* s_wcap, int* s_err, int* s_nseg, int* s_n, int* s_ser,
+                                  long long* cnt, int spec_block, int* spec_cool, int run_limit = SERIAL_RUN) {
   const int lane = lane_id();
-  const int Wt = ws.Wt, marg = ws.marg;
+  const int marg = ws.marg;
+  const int row = ws.Wt << 4;
   const Batch B0 = *s_B;
-  long long pops = 0, pushes = 0;
-  int run = 0;
-  const long long cool_lim = (spec_cool && *spec_cool > 0) ? *spec_cool : (1ll << 62);
-  int lo = lowest_bucket(s_head, s_tail, 0);
-  int ring = 0, ring_l = -1, ring_h0 = 0, ring_n = 0;
+  const unsigned qcap32 = (unsigned)min(ws.qcap, (long long)0x7fffffff);
+  int pops = 0, pushes = 0, run = 0;
+  const int cool_lim = (spec_cool && *spec_cool > 0) ? *spec_cool : 0x7fffffff;
+  int lo = __builtin_amdgcn_readfirstlane(lowest_bucket(s_head, s_tail, 0));
+  int cl = -1, ch = 0, cb = 0;  // the bucket being popped: level, head (in a register), queue base
+  int ring = 0, ring_h0 = 0, ring_end = 0;
   while (lo < NQ) {
-    const int h = s_head[lo], navail = s_tail[lo] - h;
-    if (navail <= 0) {
-      lo = lowest_bucket(s_head, s_tail, lo + 1);
-      continue;
+    if (lo != cl) {  // switch buckets (every lane stores the same value: no divergent branch)
+      if (cl >= 0) s_head[cl] = ch;
+      wave_sync();
+      cl = lo;
+      ch = __builtin_amdgcn_readfirstlane(s_head[lo]);
+      cb = __builtin_amdgcn_readfirstlane(s_qbase[lo]);
+      ring_end = ch;  // the ring is refilled before the first pop
+    }
+    if (ch >= ring_end) {  // the ring ran out: the bucket's tail decides
+      const int ct = __builtin_amdgcn_readfirstlane(s_tail[cl]);
+      if (ch >= ct) {  // empty: the next one up (LDS is current but for cl's head)
+        s_head[cl] = ch;
+        wave_sync();
+        cl = -1;
+        lo = __builtin_amdgcn_readfirstlane(lowest_bucket(s_head, s_tail, lo + 1));
+        continue;
+      }
+      ring_h0 = ch;  // its next 64 slots, one load per lane
+      ring_end = ch + min(ct - ch, 64);
+      ring = (ch + lane < ring_end) ? ld_qbuf_v(ws, cb + ch + lane) : 0;
+      vm_drain();
     }
     if (run >= run_limit) break;
     if (spec_block > 0 && lo >= spec_block) break;  // the cascade that stopped the speculative engine is done
@@ -2411,68 +2438,84 @@ __device__ void serial_loop(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_q
     // the speculative engine is being allocated (first entry into this regime): return soon, so
     // that the launches that carry it take the regime over
     if (ws.spec_lazy && pops >= 4096) break;
-    if (lo != ring_l || h >= ring_h0 + ring_n) {  // the bucket's next 64 slots, one load per lane
-      ring_l = lo;
-      ring_h0 = h;
-      ring_n = min(navail, 64);
-      ring = (lane < ring_n) ? ld_qbuf_v(ws, s_qbase[lo] + h + lane) : 0;
-      // the ring is waited for here, once per refill: left to the compiler, the wait sits at the
-      // readlane below on EVERY pop, as vmcnt(0) behind the previous pop's label and queue stores
-      vm_drain();
-    }
-    const int p = __builtin_amdgcn_readlane(ring, h - ring_h0);  // a uniform lane: no LDS crossbar
+    const int p = __builtin_amdgcn_readlane(ring, ch - ring_h0);
+    // lane d < 4: neighbour d of tiled pixel pb is pb + (((pb & msk) != val) ? dn : dw) (nbi).
+    // RELANE (k_scan, whose long-lived registers leave none for these): recomputed on every pop
+    // from a lane id the compiler cannot hoist, instead of reloaded from scratch
+    int lid = lane;
+    if (RELANE) asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0" : "=v"(lid));
+    const bool nbl = lid < 4;
+    const unsigned d8 = (unsigned)(lid & 3) << 3;  // the lane's byte of the packed per-direction constants
+    const int msk = (int)__builtin_amdgcn_ubfe(0x0C0C0303u, d8, 8);
+    const int val = (int)__builtin_amdgcn_ubfe(0x0C000300u, d8, 8);
+    const int dn = __builtin_amdgcn_sbfe(0x04FC01FF, d8, 8);
+    const int dw = (d8 < 16) ? __builtin_amdgcn_sbfe(0x00000DF3, d8, 8) : ((d8 == 16) ? 12 - row : row - 12);
+    const int* ldbase = nbl ? ws.mk : ws.w4;
     const int pb = p + marg;
-    int nb[4], st[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      nb[d] = nbi(pb, d, Wt) - marg;
-      st[d] = ld_state_v(ws, nb[d]);
-    }
-    const unsigned w4 = (unsigned)ws.w4[p];
-    int lab = 0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-      if (st[d] > 0) lab = fold_lab(lab, st[d]);
-    if (lab == 0) {  // impossible for an exact queue
+    const int idx = nbl ? pb + (((pb & msk) != val) ? dn : dw) - marg : p;
+    const int v = __hip_atomic_load(ldbase + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const unsigned w4 = (unsigned)__builtin_amdgcn_readlane(v, 4);
+    // the fold of the settled neighbours (fold_lab in direction order): 0 if none, their label if
+    // they agree, WSHED otherwise -- i.e. from their largest and smallest label
+    const bool pos = nbl && v > 0;
+    int mx = pos ? v : 0, mn = pos ? v : 0x7fffffff;
+    mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+    mn = min(mn, __builtin_amdgcn_update_dpp(0x7fffffff, mn, 0xB1, 0xF, 0xF, false));
+    mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+    mn = min(mn, __builtin_amdgcn_update_dpp(0x7fffffff, mn, 0x4E, 0xF, 0xF, false));
+    const int smx = __builtin_amdgcn_readfirstlane(mx), smn = __builtin_amdgcn_readfirstlane(mn);
+    int lab = (smx == 0) ? 0 : (smx == smn ? smx : WSHED);
+    const bool bad = lab == 0;  // impossible for an exact queue
+    if (bad) {
       *s_err = ERR_STATE;
       lab = WSHED;
     }
-    // every lane stores the same value to the same address (one request): a later load by the
-    // wave includes the lane's own earlier store, so no wait is needed for the next pop to see it
-    st_state(ws, p, lab);
-    s_head[lo] = h + 1;
+    ++ch;
     ++pops;
-    bool lower = false;
+    // pushing lanes: neighbours in state 0 of a labelled pixel
+    const bool push = nbl && v == 0 && lab != WSHED;
+    const unsigned pm = (unsigned)__ballot(push);
+    int sv = lab;  // lanes >= 4: the popped pixel's label (idx == p)
     int newlo = lo;
-    if (lab != WSHED) {
+    bool ok = !nbl;  // lanes that store a state
+    if (pm) {
+      const int t = (int)__builtin_amdgcn_ubfe(w4, d8, 8);
+      const int qb = s_qbase[t], qt = s_tail[t];
+      int rank = 0;  // earlier pushing lanes of the same bucket (direction order)
+      if (pm & (pm - 1)) {
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        if (st[d] != 0) continue;
-        const int t = (int)((w4 >> (8 * d)) & 255u);
-        const int dest = s_qbase[t] + s_tail[t];
-        if (dest < 0 || (long long)dest >= ws.qcap) {
-          *s_err = ERR_CAPACITY;
-          continue;
-        }
-        ws.qbuf[dest] = nb[d];
-        st_state(ws, nb[d], queued_state(dest));
-        s_tail[t] = s_tail[t] + 1;
-        ++pushes;
-        if (t < lo) lower = true;
-        newlo = min(newlo, t);
+        for (int e = 0; e < 3; ++e)
+          rank += (((pm >> e) & 1u) && e < lane && (int)((w4 >> (8 * e)) & 255u) == t) ? 1 : 0;
       }
+      const int dest = qb + qt + rank;
+      if (__ballot(push && (unsigned)dest >= qcap32)) {
+        *s_err = ERR_CAPACITY;
+        break;
+      }
+      atomicAdd(&s_tail[t], push ? 1 : 0);  // (adds commute; lanes of the same bucket each add 1)
+      pushes += __builtin_popcount(pm);
+      int tm = push ? t : NQ;
+      tm = min(tm, __builtin_amdgcn_update_dpp(NQ, tm, 0xB1, 0xF, 0xF, false));
+      tm = min(tm, __builtin_amdgcn_update_dpp(NQ, tm, 0x4E, 0xF, 0xF, false));
+      newlo = min(lo, __builtin_amdgcn_readfirstlane(tm));
+      sv = push ? queued_state(dest) : lab;
+      ok = ok || push;
+      if (push) ws.qbuf[dest] = idx;
     }
-    run = lower ? 0 : run + 1;
+    // the popped pixel's label and the pushed neighbours' queue states: one store
+    if (ok) ws.mk[idx] = sv;
+    run = (newlo < lo) ? 0 : run + 1;
     lo = newlo;
-    if (*s_err) break;
+    if (bad) break;
   }
+  if (cl >= 0) s_head[cl] = ch;
   wave_sync();
   if (lane == 0) {
     cnt[0] += pops;
     cnt[1] += pops;
     cnt[2] += pushes;
-    *s_wcap = 0;  // the next batch: a whole generation (next_wcap shrinks it again on a cut)
-    if (spec_cool && *spec_cool > 0) *spec_cool = (int)max(0ll, (long long)*spec_cool - pops);
+    *s_wcap = 0;  // the next batch: a whole generation
+    if (spec_cool && *spec_cool > 0) *spec_cool = max(0, *spec_cool - pops);
   }
   wave_sync();
   form_batch(s_qbase, s_head, s_tail, 0, 0, s_seg, s_nseg, s_n);
@@ -2544,8 +2587,8 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
         } else if (s_ser) {
           if (ws.spec_lazy && lane == 0) ctl->spec_want = 1;  // the host allocates the engine
           const unsigned long long t0 = ws.diag ? __builtin_amdgcn_s_memrealtime() : 0;
-          serial_loop(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, c4,
-                      s_specblk > 0 ? s_specblk : 0, s_specblk >= 0 ? &s_specool : nullptr);
+          serial_loop_lanes<true>(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, c4,
+                            s_specblk > 0 ? s_specblk : 0, s_specblk >= 0 ? &s_specool : nullptr);
           if (ws.spec_lazy && lane == 0) s_lazyx = 1;
           if (ws.diag && lane == 0) {
             atomicAdd(&ws.diag[19], (unsigned long long)c4[0]);
@@ -2781,151 +2824,6 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
   }
 }
 
-// serial_loop_lanes: serial_loop's pops for a wave that has its flood to itself (k_serial_multi),
-// with the pop's memory work spread over lanes: lane d < 4 loads the state of neighbour d and the
-// other lanes the pixel's weights, in ONE load instruction; a pop's pushes are one store of queue
-// slots and one of states (the popped pixel's label in the same instruction, lanes >= 4), their
-// slots ranked among the pushing lanes in direction order (cv::watershed's push order).  The head
-// of the popped bucket stays in a register while the loop stays on it; its next 64 slots sit in
-// a register ring, so a pop only looks at the bucket's tail when the ring runs out.  Same pops,
-// same order, same states as serial_loop, whose pop is ~180 instructions of scalar address
-// arithmetic and an LDS round trip per push, issued one at a time by a lone wave (round 6: 92
-// notConnectedMarkers floods of one 1024^2 image 134 -> 170 Mpx/s, profiles/r06k_ab_serial_lanes.log).
-// Values the loop branches on are read from LDS through readfirstlane (and no store sits in a
-// lane-divergent branch of its own): otherwise the compiler keeps them in vector registers and
-// turns every branch of the loop into exec-mask code.
-__device__ void serial_loop_lanes(const Ws& ws, Batch* s_B, Seg* s_seg, const int* s_qbase, int* s_head,
-                                  int* s_tail, int* s_wcap, int* s_err, int* s_nseg, int* s_n, int* s_ser,
-                                  long long* cnt, int run_limit) {
-  const int lane = lane_id();
-  const int marg = ws.marg;
-  const int row = ws.Wt << 4;
-  const Batch B0 = *s_B;
-  // lane d < 4: neighbour d of tiled pixel pb is pb + (((pb & msk) != val) ? dn : dw) (nbi)
-  const int d = lane & 3;
-  const int msk = (d < 2) ? 3 : 12;
-  const int val = (d == 0) ? 0 : (d == 1) ? 3 : (d == 2) ? 0 : 12;
-  const int dn = (d == 0) ? -1 : (d == 1) ? 1 : (d == 2) ? -4 : 4;
-  const int dw = (d == 0) ? -13 : (d == 1) ? 13 : (d == 2) ? 12 - row : row - 12;
-  const bool nbl = lane < 4;
-  const int* ldbase = nbl ? ws.mk : ws.w4;
-  const unsigned qcap32 = (unsigned)min(ws.qcap, (long long)0x7fffffff);
-  int pops = 0, pushes = 0, run = 0;
-  int lo = __builtin_amdgcn_readfirstlane(lowest_bucket(s_head, s_tail, 0));
-  int cl = -1, ch = 0, cb = 0;  // the bucket being popped: level, head (in a register), queue base
-  int ring = 0, ring_h0 = 0, ring_end = 0;
-  while (lo < NQ) {
-    if (lo != cl) {  // switch buckets (every lane stores the same value: no divergent branch)
-      if (cl >= 0) s_head[cl] = ch;
-      wave_sync();
-      cl = lo;
-      ch = __builtin_amdgcn_readfirstlane(s_head[lo]);
-      cb = __builtin_amdgcn_readfirstlane(s_qbase[lo]);
-      ring_end = ch;  // the ring is refilled before the first pop
-    }
-    if (ch >= ring_end) {  // the ring ran out: the bucket's tail decides
-      const int ct = __builtin_amdgcn_readfirstlane(s_tail[cl]);
-      if (ch >= ct) {  // empty: the next one up (LDS is current but for cl's head)
-        s_head[cl] = ch;
-        wave_sync();
-        cl = -1;
-        lo = __builtin_amdgcn_readfirstlane(lowest_bucket(s_head, s_tail, lo + 1));
-        continue;
-      }
-      ring_h0 = ch;  // its next 64 slots, one load per lane
-      ring_end = ch + min(ct - ch, 64);
-      ring = (ch + lane < ring_end) ? ld_qbuf_v(ws, cb + ch + lane) : 0;
-      vm_drain();
-    }
-    if (run >= run_limit) break;
-    if (ws.spec_lazy && pops >= 4096) break;
-    const int p = __builtin_amdgcn_readlane(ring, ch - ring_h0);
-    const int pb = p + marg;
-    const int idx = nbl ? pb + (((pb & msk) != val) ? dn : dw) - marg : p;
-    const int v = __hip_atomic_load(ldbase + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const unsigned w4 = (unsigned)__builtin_amdgcn_readlane(v, 4);
-    // the fold of the settled neighbours (fold_lab in direction order): 0 if none, their label if
-    // they agree, WSHED otherwise -- i.e. from their largest and smallest label
-    const bool pos = nbl && v > 0;
-    int mx = pos ? v : 0, mn = pos ? v : 0x7fffffff;
-    mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
-    mn = min(mn, __builtin_amdgcn_update_dpp(0x7fffffff, mn, 0xB1, 0xF, 0xF, false));
-    mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
-    mn = min(mn, __builtin_amdgcn_update_dpp(0x7fffffff, mn, 0x4E, 0xF, 0xF, false));
-    const int smx = __builtin_amdgcn_readfirstlane(mx), smn = __builtin_amdgcn_readfirstlane(mn);
-    int lab = (smx == 0) ? 0 : (smx == smn ? smx : WSHED);
-    const bool bad = lab == 0;  // impossible for an exact queue
-    if (bad) {
-      *s_err = ERR_STATE;
-      lab = WSHED;
-    }
-    ++ch;
-    ++pops;
-    // pushing lanes: neighbours in state 0 of a labelled pixel
-    const bool push = nbl && v == 0 && lab != WSHED;
-    const unsigned pm = (unsigned)__ballot(push);
-    int sv = lab;  // lanes >= 4: the popped pixel's label (idx == p)
-    int newlo = lo;
-    bool ok = !nbl;  // lanes that store a state
-    if (pm) {
-      const int t = (int)((w4 >> (8 * d)) & 255u);
-      const int qb = s_qbase[t], qt = s_tail[t];
-      int rank = 0;  // earlier pushing lanes of the same bucket (direction order)
-      if (pm & (pm - 1)) {
-#pragma unroll
-        for (int e = 0; e < 3; ++e)
-          rank += (((pm >> e) & 1u) && e < lane && (int)((w4 >> (8 * e)) & 255u) == t) ? 1 : 0;
-      }
-      const int dest = qb + qt + rank;
-      if (__ballot(push && (unsigned)dest >= qcap32)) {
-        *s_err = ERR_CAPACITY;
-        break;
-      }
-      atomicAdd(&s_tail[t], push ? 1 : 0);  // (adds commute; lanes of the same bucket each add 1)
-      pushes += __builtin_popcount(pm);
-      int tm = push ? t : NQ;
-      tm = min(tm, __builtin_amdgcn_update_dpp(NQ, tm, 0xB1, 0xF, 0xF, false));
-      tm = min(tm, __builtin_amdgcn_update_dpp(NQ, tm, 0x4E, 0xF, 0xF, false));
-      newlo = min(lo, __builtin_amdgcn_readfirstlane(tm));
-      sv = push ? queued_state(dest) : lab;
-      ok = ok || push;
-      if (push) ws.qbuf[dest] = idx;
-    }
-    // the popped pixel's label and the pushed neighbours' queue states: one store
-    if (ok) ws.mk[idx] = sv;
-    run = (newlo < lo) ? 0 : run + 1;
-    lo = newlo;
-    if (bad) break;
-  }
-  if (cl >= 0) s_head[cl] = ch;
-  wave_sync();
-  if (lane == 0) {
-    cnt[0] += pops;
-    cnt[1] += pops;
-    cnt[2] += pushes;
-    *s_wcap = 0;  // the next batch: a whole generation
-  }
-  wave_sync();
-  form_batch(s_qbase, s_head, s_tail, 0, 0, s_seg, s_nseg, s_n);
-  wave_sync();
-  if (lane == 0) {
-    Batch nb;
-    nb.mode = 0;
-    nb.epoch = B0.epoch + 1;
-    nb.ncommit = 0;
-    nb.nchunk = 0;
-    nb.rrun = 0;
-    nb.nseg = *s_nseg;
-    nb.n = (*s_nseg > 0) ? *s_n : 0;
-    nb.L = (*s_nseg > 0) ? s_seg[0].L : -1;
-    nb.bstart = (*s_nseg > 0) ? s_seg[0].bstart : 0;
-    *s_B = nb;
-    *s_ser = 0;
-    cnt[3] += pops;
-  }
-  wave_sync();
-}
-
 // ---------------------------------------------------------------------------------------------
 // k_serial_multi: the serial pops of MANY floods in one launch (the batch entry points' many-floods
 // mode, msg_set_batch_floods): block f = one wave = flood f, each flood in its own workspace
@@ -2933,7 +2831,7 @@ __device__ void serial_loop_lanes(const Ws& ws, Batch* s_B, Seg* s_seg, const in
 // -- chains of dependent pops, a lone wave's memory latency per pop -- so a
 // batch of such frames is bound by the number of floods in flight: here every flood of the call
 // (hundreds), instead of the 4-8 streams over which the full engine's floods overlap.  Each wave
-// runs the small-batch loop's serial pops (serial_loop) on its flood from wherever it stands
+// runs the serial pops (serial_loop_lanes) on its flood from wherever it stands
 // (after phase 1, or after a batch of the full engine) until its queue is empty, or until
 // run_limit consecutive pops pushed nothing below their own level (batches pay again: the host
 // finishes that flood with the full engine), then writes the queue state back and forms the next
@@ -2977,8 +2875,8 @@ __global__ __launch_bounds__(64) void k_serial_multi(const Ws* __restrict__ wss,
   }
   wave_sync();
   long long cnt[4] = {0, 0, 0, 0};
-  serial_loop_lanes(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, cnt,
-                    run_limit);
+  serial_loop_lanes<false>(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, cnt,
+                           0, nullptr, run_limit);
   wave_sync();
   for (int k = lane; k < NQ; k += 64) {
     ctl->qhead[k] = s_head[k];
