@@ -139,7 +139,9 @@ int  msg_get_kernel_profile(msg_ctx* ctx, msg_kernel_profile* out, int max_entri
  * batches (65..4096 items).
  * enable == 4 (the -DMSEG_SPEC_PROF diagnostic build) reports the wave-cooperative cascade
  * pop's phases instead (s_memtime cycles summed over pops): loads issued + queue fix, the wait
- * for the loads, writes + decision, pushes, select; counters 5..7 are 0. */
+ * for the loads, writes + decision, pushes, select; counters 5..7 are 0.  In the -DMSEG_SER_PROF
+ * diagnostic build it reports the serial pops' phases (s_memtime cycles summed over pops): load,
+ * fold, push, between pops, pushes, pops, ring-refill cycles, empty-bucket-scan cycles. */
 int  msg_set_diag(msg_ctx* ctx, int enable);
 /* Speculative generations for the interrupt-dense regime (textured frames, scattered seeds):
  * on by default.  enable = 0 keeps the batch engine's serial pops there instead (A/B runs and

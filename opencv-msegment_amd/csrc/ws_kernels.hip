@@ -2409,10 +2409,16 @@ __device__ void serial_loop_lanes(const Ws& ws, Batch* s_B, Seg* s_seg, const in
   int lo = __builtin_amdgcn_readfirstlane(lowest_bucket(s_head, s_tail, 0));
   int cl = -1, ch = 0, cb = 0;  // the bucket being popped: level, head (in a register), queue base
   int ring = 0, ring_h0 = 0, ring_end = 0;
+#ifdef MSEG_SER_PROF
+  unsigned long long ph[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tprev = 0;  // load, fold, push, between, pushes, switches, refills, refill cycles, scan cycles
+#endif
   while (lo < NQ) {
     if (lo != cl) {  // switch buckets (every lane stores the same value: no divergent branch)
       if (cl >= 0) s_head[cl] = ch;
       wave_sync();
+#ifdef MSEG_SER_PROF
+      ph[5] += 1;
+#endif
       cl = lo;
       ch = __builtin_amdgcn_readfirstlane(s_head[lo]);
       cb = __builtin_amdgcn_readfirstlane(s_qbase[lo]);
@@ -2421,16 +2427,29 @@ __device__ void serial_loop_lanes(const Ws& ws, Batch* s_B, Seg* s_seg, const in
     if (ch >= ring_end) {  // the ring ran out: the bucket's tail decides
       const int ct = __builtin_amdgcn_readfirstlane(s_tail[cl]);
       if (ch >= ct) {  // empty: the next one up (LDS is current but for cl's head)
+#ifdef MSEG_SER_PROF
+        const unsigned long long E0 = __builtin_amdgcn_s_memtime();
+#endif
         s_head[cl] = ch;
         wave_sync();
         cl = -1;
         lo = __builtin_amdgcn_readfirstlane(lowest_bucket(s_head, s_tail, lo + 1));
+#ifdef MSEG_SER_PROF
+        ph[8] += __builtin_amdgcn_s_memtime() - E0 + (unsigned)(lo & 0);
+#endif
         continue;
       }
+#ifdef MSEG_SER_PROF
+      ph[6] += 1;
+      const unsigned long long R0 = __builtin_amdgcn_s_memtime();
+#endif
       ring_h0 = ch;  // its next 64 slots, one load per lane
       ring_end = ch + min(ct - ch, 64);
       ring = (ch + lane < ring_end) ? ld_qbuf_v(ws, cb + ch + lane) : 0;
       vm_drain();
+#ifdef MSEG_SER_PROF
+      ph[7] += __builtin_amdgcn_s_memtime() - R0 + (unsigned)(__builtin_amdgcn_readfirstlane(ring) & 0);
+#endif
     }
     if (run >= run_limit) break;
     if (spec_block > 0 && lo >= spec_block) break;  // the cascade that stopped the speculative engine is done
@@ -2438,6 +2457,10 @@ __device__ void serial_loop_lanes(const Ws& ws, Batch* s_B, Seg* s_seg, const in
     // the speculative engine is being allocated (first entry into this regime): return soon, so
     // that the launches that carry it take the regime over
     if (ws.spec_lazy && pops >= 4096) break;
+#ifdef MSEG_SER_PROF
+    const unsigned long long T0 = __builtin_amdgcn_s_memtime();
+    if (tprev) ph[3] += T0 - tprev;
+#endif
     const int p = __builtin_amdgcn_readlane(ring, ch - ring_h0);
     // lane d < 4: neighbour d of tiled pixel pb is pb + (((pb & msk) != val) ? dn : dw) (nbi).
     // RELANE (k_scan, whose long-lived registers leave none for these): recomputed on every pop
@@ -2455,6 +2478,10 @@ __device__ void serial_loop_lanes(const Ws& ws, Batch* s_B, Seg* s_seg, const in
     const int idx = nbl ? pb + (((pb & msk) != val) ? dn : dw) - marg : p;
     const int v = __hip_atomic_load(ldbase + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const unsigned w4 = (unsigned)__builtin_amdgcn_readlane(v, 4);
+#ifdef MSEG_SER_PROF
+    const unsigned long long T1 = __builtin_amdgcn_s_memtime() + (w4 & 0u);
+    ph[0] += T1 - T0;
+#endif
     // the fold of the settled neighbours (fold_lab in direction order): 0 if none, their label if
     // they agree, WSHED otherwise -- i.e. from their largest and smallest label
     const bool pos = nbl && v > 0;
@@ -2470,6 +2497,10 @@ __device__ void serial_loop_lanes(const Ws& ws, Batch* s_B, Seg* s_seg, const in
       *s_err = ERR_STATE;
       lab = WSHED;
     }
+#ifdef MSEG_SER_PROF
+    const unsigned long long T2 = __builtin_amdgcn_s_memtime() + (unsigned)(lab & 0);
+    ph[1] += T2 - T1;
+#endif
     ++ch;
     ++pops;
     // pushing lanes: neighbours in state 0 of a labelled pixel
@@ -2504,12 +2535,25 @@ __device__ void serial_loop_lanes(const Ws& ws, Batch* s_B, Seg* s_seg, const in
     }
     // the popped pixel's label and the pushed neighbours' queue states: one store
     if (ok) ws.mk[idx] = sv;
+#ifdef MSEG_SER_PROF
+    tprev = __builtin_amdgcn_s_memtime() + (unsigned)(newlo & 0);
+    ph[2] += tprev - T2;
+    ph[4] += __builtin_popcount(pm);
+#endif
     run = (newlo < lo) ? 0 : run + 1;
     lo = newlo;
     if (bad) break;
   }
   if (cl >= 0) s_head[cl] = ch;
   wave_sync();
+#ifdef MSEG_SER_PROF
+  if (ws.diag && lane == 0) {
+    for (int k = 0; k < 5; ++k) atomicAdd(&ws.diag[24 + k], ph[k]);
+    atomicAdd(&ws.diag[29], (unsigned long long)pops);
+    atomicAdd(&ws.diag[30], ph[7]);
+    atomicAdd(&ws.diag[31], ph[8]);
+  }
+#endif
   if (lane == 0) {
     cnt[0] += pops;
     cnt[1] += pops;
