@@ -46,6 +46,7 @@ struct msg_ctx {
   int32_t *d_qbuf = nullptr, *d_ilist = nullptr;
   int32_t *d_cnt = nullptr, *d_coff = nullptr, *d_tot = nullptr, *d_choff = nullptr;
   unsigned* d_capp = nullptr;  // CAP_SLOTS x NQ
+  bool capp_clean = false;     // d_capp is zero (k_init_scan clears it after reading it)
   unsigned long long *d_tl = nullptr, *d_desc = nullptr, *d_cflag = nullptr;
   long long qcap = 0;
   // speculative generations (spec_kernels.hip): allocated on the first flood that may use them
@@ -73,6 +74,8 @@ struct msg_ctx {
   int* h_mir = nullptr;
   int* d_mir = nullptr;  // its device address
   Ctl* h_tail = nullptr;  // pinned copy of the control block read back at the end of a flood
+  Ctl* d_tail = nullptr;  // its device address (k_tail writes it)
+  int tail_seq = 0;       // k_tail's last release into h_mir[7]
   // ordering with the legacy null stream for device calls given stream = NULL (StreamScope)
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   unsigned epoch = 1;
@@ -330,6 +333,7 @@ int ensure_flood(msg_ctx* c, int H, int W, hipStream_t st) {
   HIPCHK(c, hipMalloc((void**)&c->d_tot, rc * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_choff, rc * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_capp, (size_t)CAP_SLOTS * NQ * 4));
+  c->capp_clean = false;
   HIPCHK(c, hipMemsetAsync(c->d_tl, 0, n * 8, st));
   HIPCHK(c, hipMalloc((void**)&c->d_cflag, (size_t)(n / RBS + 2) * 16));
   HIPCHK(c, hipMemsetAsync(c->d_cflag, 0, (size_t)(n / RBS + 2) * 16, st));
@@ -378,20 +382,21 @@ int check_size(msg_ctx* c, int rows, int cols, bool flood = false) {
 
 // Spin on the host-mapped progress mirror until iteration `target` has reported.  A stream that
 // drains (or fails) without the report ends the wait with an error instead of spinning forever.
-int wait_progress(msg_ctx* c, hipStream_t st, int target) {
+int wait_mirror(msg_ctx* c, hipStream_t st, int word, int target) {
   for (unsigned spins = 1;; ++spins) {
-    if (__atomic_load_n(&c->h_mir[0], __ATOMIC_ACQUIRE) >= target) return MSG_OK;
+    if (__atomic_load_n(&c->h_mir[word], __ATOMIC_ACQUIRE) >= target) return MSG_OK;
     if ((spins & 4095) == 0) {
       const hipError_t q = hipStreamQuery(st);
       if (q == hipSuccess) {
-        if (__atomic_load_n(&c->h_mir[0], __ATOMIC_ACQUIRE) >= target) return MSG_OK;
-        return fail(c, MSG_ESTATE, "stream drained before iteration %d reported", target);
+        if (__atomic_load_n(&c->h_mir[word], __ATOMIC_ACQUIRE) >= target) return MSG_OK;
+        return fail(c, MSG_ESTATE, "stream drained before mirror word %d reached %d", word, target);
       }
       if (q != hipErrorNotReady) return fail(c, MSG_EHIP, "flood stream: %s", hipGetErrorString(q));
     }
     __builtin_ia32_pause();
   }
 }
+int wait_progress(msg_ctx* c, hipStream_t st, int target) { return wait_mirror(c, st, 0, target); }
 
 // A flood in progress on a context: its kernel arguments and the host loop's regime flags.
 struct FloodRun {
@@ -497,10 +502,13 @@ int flood_begin(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int H,
   bind_spec(c, fr, fr.spec_bound);
   const int npx = (int)((N + CH - 1) / CH);
   const int gsc = std::min(npx * (CH / 1024), 1024);
-  HIPCHK(c, hipMemsetAsync(c->d_ctl, 0, sizeof(Ctl), st));
-  HIPCHK(c, hipMemsetAsync(c->d_capp, 0, (size_t)CAP_SLOTS * NQ * 4, st));
+  // the control block and the level histograms are zeroed by the phase-0 kernel (prep_zero), the
+  // capacity histograms by k_init_scan after reading them: a host memset only when a flood
+  // stopped in between (or the buffer is new)
+  if (!c->capp_clean) HIPCHK(c, hipMemsetAsync(c->d_capp, 0, (size_t)CAP_SLOTS * NQ * 4, st));
+  c->capp_clean = false;
   if (c->diag) HIPCHK(c, hipMemsetAsync(c->d_diag, 0, 32 * sizeof(unsigned long long), st));
-  HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, (size_t)npx * NQ * sizeof(int32_t), st));
+  (void)npx;
   const int nrc = H * ws.nseg;  // raster chunks
   // k_prep4 (one thread per tile) where widths and buffers allow 12-B / 16-B quad loads
   if (W % 4 == 0 && ((uintptr_t)d_img & 3) == 0 && ((uintptr_t)d_mk_in & 15) == 0)
@@ -508,6 +516,7 @@ int flood_begin(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int H,
   else
     LAUNCH(c, KID_PREP, st, k_prep, dim3((H + 3) / 4 * ws.nseg), dim3(RSEG), 0, ws, d_mk_in);
   LAUNCH(c, KID_INIT_SCAN, st, k_init_scan, dim3(1), dim3(1024), 0, ws, nrc, c->epoch, c->stag);
+  c->capp_clean = hipPeekAtLastError() == hipSuccess;
   LAUNCH(c, KID_COMPACT, st, k_compact, dim3((nrc + 4 * CPW - 1) / (4 * CPW)), dim3(256), 0, ws, nrc);
   LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
   LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, -1);
@@ -621,11 +630,22 @@ int flood_end(msg_ctx* c, FloodRun& fr, int32_t* d_labels, int depth = 0, const 
            depth, d_pal, d_dst, d_gray, &c->d_ctl->error);
     HIPCHK(c, hipGetLastError());
   }
-  // into pinned memory: a copy to pageable memory is staged and synchronous on its own
-  HIPCHK(c, hipMemcpyAsync(c->h_tail, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
   unsigned long long dgv[32] = {0};
-  if (c->diag) HIPCHK(c, hipMemcpyAsync(dgv, c->d_diag, sizeof(dgv), hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipStreamSynchronize(st));
+  if (c->diag || c->prof) {  // (the counters' copy and the profile's events want the stream drained)
+    // into pinned memory: a copy to pageable memory is staged and synchronous on its own
+    HIPCHK(c, hipMemcpyAsync(c->h_tail, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
+    if (c->diag) HIPCHK(c, hipMemcpyAsync(dgv, c->d_diag, sizeof(dgv), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+  } else {
+    const int seq = ++c->tail_seq;
+    LAUNCH(c, KID_UNTILE, st, k_tail, dim3(1), dim3(256), 0, c->d_ctl, c->d_tail, c->d_mir, seq);
+    HIPCHK(c, hipGetLastError());
+    const int rc = wait_mirror(c, st, 7, seq);
+    if (rc) {
+      (void)hipStreamSynchronize(st);
+      return rc;
+    }
+  }
   const Ctl& tail = *c->h_tail;
   c->stats.host_syncs += 1;
   if (c->prof) collect_profile(c);
@@ -1125,12 +1145,14 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
       hipHostMalloc((void**)&c->h_mir, 8 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer((void**)&c->d_mir, c->h_mir, 0) != hipSuccess ||
-      hipHostMalloc((void**)&c->h_tail, sizeof(Ctl), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_tail, sizeof(Ctl), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&c->d_tail, c->h_tail, 0) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming) != hipSuccess) {
     msg_destroy(c);
     return MSG_EHIP;
   }
+  for (int k = 0; k < 8; ++k) c->h_mir[k] = 0;  // (word 7: k_tail's releases start at 1)
   {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->dev) != hipSuccess ||

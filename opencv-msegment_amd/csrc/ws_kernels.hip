@@ -211,6 +211,21 @@ constexpr int PREP_RAW = (3 * PREP_COLS + 8) / 4 + 1;  // dwords of one BGR row 
 
 // thread = one tile row (4 pixels): tile tid >> 2, row tid & 3, so 4 consecutive lanes write one
 // whole 128-B tile line; frames are < 2^29 pixels, so 32-bit offsets (3N < 2^31) suffice.
+// The flood's zeroed state, written by the phase-0 kernel instead of two host memsets ahead of
+// it (≈5 µs and a dependent launch each): the control block (block 0) and the per-chunk level
+// histograms (a slice per block).  Neither is read before the next kernel.
+__device__ __forceinline__ void prep_zero(const Ws& ws) {
+  const int G = gridDim.x, b = blockIdx.x, T = blockDim.x, t = threadIdx.x;
+  if (b == 0) {
+    int* p = reinterpret_cast<int*>(ws.ctl);
+    for (int k = t; k < (int)(sizeof(Ctl) / 4); k += T) p[k] = 0;
+  }
+  const long long ncnt = ((ws.N + CH - 1) / CH) * NQ;
+  const long long per = (ncnt + G - 1) / G;
+  const long long e = min((long long)(b + 1) * per, ncnt);
+  for (long long k = (long long)b * per + t; k < e; k += T) ws.cnt[k] = 0;
+}
+
 __global__ __launch_bounds__(RSEG) void k_prep(Ws ws, const int32_t* __restrict__ mk_in) {
   static_assert(RSEG >= NQ && RSEG % 64 == 0 && PREP_RAW <= RSEG, "strip = RSEG/4 tiles x 4 rows = RSEG threads");
   __shared__ unsigned caph[NQ];
@@ -224,6 +239,7 @@ __global__ __launch_bounds__(RSEG) void k_prep(Ws ws, const int32_t* __restrict_
   const int r0 = tr * 4, x0 = cs * RSEG;
   const int ncol = min(RSEG, W - x0) + 2;  // strip column j <-> image column x0 - 1 + j
   const int nbytes = 3 * H * W;
+  prep_zero(ws);
   if (tid < NQ) caph[tid] = 0;
   // ---- stage rows r0-1..r0+4: all loads issued before the first LDS store ----
   const bool aligned = (((uintptr_t)ws.img) & 3) == 0;
@@ -477,6 +493,7 @@ __global__ __launch_bounds__(PREP4_T) void k_prep4(Ws ws, const int32_t* __restr
   Prep4Row rw[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) rw[i] = prep4_load(ws, mk_in, r0 - 1 + i, c0, tin, halo, hc);
+  prep_zero(ws);  // (stores issued while the loads are in flight)
   uint32_t px[6][4];
   int mm[6][4];
 #pragma unroll
@@ -855,6 +872,10 @@ __global__ __launch_bounds__(1024) void k_init_scan(Ws ws, int npxchunk, unsigne
 #pragma unroll
     for (int k = 0; k < CAP_SLOTS / 4; ++k) sum += ws.capp[(g * (CAP_SLOTS / 4) + k) * NQ + lv];
     capq[g][lv] = sum;
+    // zeroed for the context's next flood once read (the host clears them itself when a flood
+    // stopped between the phase-0 kernel and this one: msg_ctx::capp_clean)
+#pragma unroll
+    for (int k = 0; k < CAP_SLOTS / 4; ++k) ws.capp[(g * (CAP_SLOTS / 4) + k) * NQ + lv] = 0;
   }
   __syncthreads();
   long long cv = 0, cx = 0;
@@ -1760,6 +1781,19 @@ __device__ void scatter_chunks(const Ws& ws, const Batch& B, int first, int stri
     }
     __syncthreads();  // before the next sub-round reuses run/wcnt
   }
+}
+
+// End of a flood: the control block into its host-mapped copy, then `seq` released into the
+// progress mirror's word 7, on which the host spins instead of synchronising the stream (the wake
+// of a stream synchronisation is a device signal; a mapped word is seen on its first read).
+__global__ __launch_bounds__(256) void k_tail(const Ctl* __restrict__ ctl, Ctl* htail, int* hmir, int seq) {
+  const int* s = reinterpret_cast<const int*>(ctl);
+  int* d = reinterpret_cast<int*>(htail);
+  for (int k = threadIdx.x; k < (int)(sizeof(Ctl) / 4); k += blockDim.x)
+    __hip_atomic_store(d + k, s[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(hmir + 7, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(1024) void k_scatter(Ws ws, int iter) {
