@@ -518,7 +518,7 @@ int flood_begin(msg_ctx* c, const uint8_t* d_img, const int32_t* d_mk_in, int H,
   LAUNCH(c, KID_INIT_SCAN, st, k_init_scan, dim3(1), dim3(1024), 0, ws, nrc, c->epoch, c->stag);
   c->capp_clean = hipPeekAtLastError() == hipSuccess;
   LAUNCH(c, KID_COMPACT, st, k_compact, dim3((nrc + 4 * CPW - 1) / (4 * CPW)), dim3(256), 0, ws, nrc);
-  LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);
+  LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws, 0);
   LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, -1);
   HIPCHK(c, hipGetLastError());
   return MSG_OK;
@@ -540,6 +540,7 @@ int flood_loop(msg_ctx* c, FloodRun& fr) {
   __atomic_store_n(&c->h_mir[0], -1, __ATOMIC_RELEASE);
   c->h_mir[4] = 0;
   c->h_mir[5] = 0;
+  c->h_mir[8] = 0;
   // the first two groups are queued before any report: assume a large flood batch (two-launch
   // iterations), as phase 1's queue usually is -- a wrong guess costs a declined commit or a small
   // batch committed by the grid instead of k_scan's loop, never a wrong result (every kernel checks
@@ -556,6 +557,8 @@ int flood_loop(msg_ctx* c, FloodRun& fr) {
   const int gflat = std::max(1, c->cus);
   for (;;) {
     const bool spec_it = fr.spec_bound && c->h_mir[4] != 0;
+    // serial pops in a kernel of their own once the flood has reached that regime
+    const bool ser_it = c->h_mir[8] != 0 && !ws.multi;
     // two-launch iterations while the last report was a large flood batch (k_commit_fast)
     const bool fast_it = !spec_it && c->fast && c->h_mir[6] != 0;
     for (int g = 0; g < c->group; ++g, ++it) {
@@ -581,7 +584,9 @@ int flood_loop(msg_ctx* c, FloodRun& fr) {
       } else {
         LAUNCH(c, KID_RESOLVE, st, k_resolve<false>, dim3(gres), dim3(RBS), 0, ws);
       }
-      LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws);  // + small batches
+      // + small batches; in the serial regime k_serial_one pops what k_scan's loop hands it
+      LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws, (ser_it && !spec_it) ? 1 : 0);
+      if (ser_it && !spec_it) LAUNCH(c, KID_SERIAL_MULTI, st, k_serial_one, dim3(1), dim3(64), 0, ws);
       LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, it);
     }
     HIPCHK(c, hipGetLastError());
@@ -1142,7 +1147,7 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
   if (hipSetDevice(c->dev) != hipSuccess ||
       hipStreamCreateWithPriority(&c->own, hipStreamNonBlocking, prio) != hipSuccess ||
       hipMalloc((void**)&c->d_ctl, sizeof(Ctl)) != hipSuccess ||
-      hipHostMalloc((void**)&c->h_mir, 8 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) !=
+      hipHostMalloc((void**)&c->h_mir, 16 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer((void**)&c->d_mir, c->h_mir, 0) != hipSuccess ||
       hipHostMalloc((void**)&c->h_tail, sizeof(Ctl), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -1152,7 +1157,7 @@ int msg_create(msg_ctx** out, int device_ordinal, unsigned flags) {
     msg_destroy(c);
     return MSG_EHIP;
   }
-  for (int k = 0; k < 8; ++k) c->h_mir[k] = 0;  // (word 7: k_tail's releases start at 1)
+  for (int k = 0; k < 16; ++k) c->h_mir[k] = 0;  // (word 7: k_tail's releases start at 1)
   {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->dev) != hipSuccess ||

@@ -1193,7 +1193,7 @@ __device__ __forceinline__ bool attempt_item(const Item& it, F fetch, int& lab_o
 // pushes to the per-chunk level histograms and the cut words, which k_scan consumes.
 __device__ Batch scan_body(const Ws& ws);
 __device__ void scatter_chunks(const Ws& ws, const Batch& B, int first, int stride);
-__device__ __forceinline__ void small_loop(const Ws& ws);
+__device__ __forceinline__ void small_loop(const Ws& ws, int ser_next);
 
 // Cold path of k_resolve's long waits (out of line, so its registers stay off the hot loop): is
 // some chunk below `chunk` neither claimed in this run nor completed?
@@ -1510,7 +1510,7 @@ __global__ __launch_bounds__(RBS) __attribute__((amdgpu_waves_per_eu(6))) void k
 // Scan (1 block x 1024) of the batch k_resolve decided; a committed batch of at most SMALL_MAX
 // items is scattered here too, and then, with nothing left for k_scatter, this block runs the
 // following small batches itself (small_loop).
-__global__ __launch_bounds__(1024) void k_scan(Ws ws) {
+__global__ __launch_bounds__(1024) void k_scan(Ws ws, int ser_next) {
   Ctl* ctl = ws.ctl;
   const Batch cb = scan_body(ws);
   if (cb.mode == 2) return;  // k_resolve gave chunks up: the batch runs again, nothing committed
@@ -1521,7 +1521,7 @@ __global__ __launch_bounds__(1024) void k_scan(Ws ws) {
   } else if (cb.nchunk > 0) {
     return;  // k_scatter commits it
   }
-  if (!ws.multi) small_loop(ws);  // a many-floods batch pops in k_serial_multi instead
+  if (!ws.multi) small_loop(ws, ser_next);  // a many-floods batch pops in k_serial_multi instead
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1807,6 +1807,7 @@ __global__ __launch_bounds__(1024) void k_scatter(Ws ws, int iter) {
     __hip_atomic_store(ws.hmir + 4, ws.ctl->spec.on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 5, ws.ctl->spec_want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir + 6, fast_batch(ws.ctl->bat, ws.ctl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ws.hmir + 8, ws.ctl->ser_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(ws.hmir, iter, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const Batch B = ws.ctl->cbat;
@@ -2616,7 +2617,7 @@ __device__ void serial_loop_lanes(const Ws& ws, Batch* s_B, Seg* s_seg, const in
   wave_sync();
 }
 
-__device__ __forceinline__ void small_loop(const Ws& ws) {
+__device__ __forceinline__ void small_loop(const Ws& ws, int ser_next) {
   constexpr int NW = 16;
   Ctl* ctl = ws.ctl;
   __shared__ int s_lab[SMALL_MAX];
@@ -2629,6 +2630,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
   __shared__ int s_specgo, s_specblk;  // hand the regime to the speculative engine; its resume level
   __shared__ int s_specool;            // regime entries to skip first (SpecCtl.cool)
   __shared__ int s_lazyx;              // leave the launch: the speculative engine is being allocated
+  __shared__ int s_sergo;              // leave the launch: k_serial_one (queued next) pops serially
   __shared__ Batch s_B;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const int Wt = ws.Wt;
@@ -2639,6 +2641,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     s_ser = 0;
     s_specgo = 0;
     s_lazyx = 0;
+    s_sergo = 0;
     s_specblk = ws.spx ? ctl->spec.block : -1;  // -1: engine off
     s_specool = ctl->spec.cool;
   }
@@ -2662,7 +2665,15 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
         long long c4[4] = {0, 0, 0, 0};
         if (s_ser && s_specblk >= 0 && s_specool <= 0 && lowest_bucket(s_head, s_tail, 0) >= s_specblk) {
           if (lane == 0) s_specgo = 1;  // interrupt-dense: speculative generations from here on
+        } else if (s_ser && ser_next) {
+          // k_serial_one, queued right after this launch, pops them with its own register budget
+          // (here the 1024-thread block's 128 VGPRs spill the loop's SGPRs into vector lanes)
+          if (lane == 0) {
+            s_sergo = 1;
+            ctl->ser_seen = 1;
+          }
         } else if (s_ser) {
+          if (lane == 0) ctl->ser_seen = 1;  // the host queues k_serial_one from now on
           if (ws.spec_lazy && lane == 0) ctl->spec_want = 1;  // the host allocates the engine
           const unsigned long long t0 = ws.diag ? __builtin_amdgcn_s_memrealtime() : 0;
           serial_loop_lanes<true>(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, c4,
@@ -2695,7 +2706,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
         }
       }
       __syncthreads();
-      if (s_specgo || s_lazyx) break;
+      if (s_specgo || s_lazyx || s_sergo) break;
       continue;
     }
     for (int k = tid; k < B.n; k += 1024) s_lab[k] = 0;
@@ -2888,6 +2899,7 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     ctl->bat = nb;
     ctl->wcap = s_wcap;
     ctl->spec.cool = s_specool;
+    if (s_sergo) ctl->ser_go = 1;
     ctl->cut = NONE;
     ctl->segcut = NONE;
     ctl->minpush = NQ;
@@ -2899,6 +2911,100 @@ __device__ __forceinline__ void small_loop(const Ws& ws) {
     ctl->lpushes += nb_push;
     if (s_err) ctl->error |= s_err;
     if (s_B.n == 0 && !s_err) ctl->done = 1;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_serial_one: the serial pops of ONE flood of the full engine, queued after k_scan while the
+// flood is in the serial regime (Ctl.ser_seen): when k_scan's small-batch loop reaches serial pops
+// it stops (Ctl.ser_go) and this one-wave kernel pops them -- the same loop as k_serial_multi's,
+// with the speculative engine's resume level and cooldown as k_scan's small-batch loop has them --
+// then hands the regime back exactly as that loop would (the next batch, or a speculative
+// generation).  A wave of its own pops at ≈0.6 µs against ≈0.8 inside k_scan, whose 1024-thread
+// block leaves the loop 128 VGPRs and spills its SGPRs into vector lanes.
+__global__ __launch_bounds__(64) void k_serial_one(Ws ws) {
+  Ctl* ctl = ws.ctl;
+  if (!ctl->ser_go) return;
+  const int lane = lane_id();
+  const Batch B0 = ctl->bat;
+  if (ctl->done || ctl->error || B0.n == 0 || B0.mode != 0) {
+    if (lane == 0) ctl->ser_go = 0;
+    return;
+  }
+  __shared__ int s_qbase[NQ], s_head[NQ], s_tail[NQ];
+  __shared__ Seg s_seg[NQ];
+  __shared__ Batch s_B;
+  __shared__ int s_wcap, s_err, s_nseg, s_n, s_ser, s_specool;
+  const int specblk = ws.spx ? ctl->spec.block : -1;  // -1: engine off
+#pragma unroll
+  for (int k = 0; k < NQ / 64; ++k) {
+    const int b = 64 * k + lane;
+    s_qbase[b] = ctl->qbase[b];
+    s_head[b] = ctl->qhead[b];
+    s_tail[b] = ctl->qtail[b];
+  }
+  if (lane == 0) {
+    s_B = B0;
+    s_wcap = 0;
+    s_err = 0;
+    s_ser = 1;
+    s_specool = ctl->spec.cool;
+    if (ws.spec_lazy) ctl->spec_want = 1;  // the host allocates the engine
+  }
+  wave_sync();
+  long long cnt[4] = {0, 0, 0, 0};
+  const unsigned long long t0 = ws.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+  serial_loop_lanes<false>(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, cnt,
+                           specblk > 0 ? specblk : 0, specblk >= 0 ? &s_specool : nullptr, SERIAL_RUN);
+  wave_sync();
+  // the cascade that stopped the speculative engine is done, or its cooldown is over: hand the
+  // regime back to it (as k_scan's small-batch loop does)
+  const bool specgo = specblk >= 0 && s_specool <= 0 && s_B.n > 0 &&
+                      __builtin_amdgcn_readfirstlane(lowest_bucket(s_head, s_tail, 0)) >= specblk;
+  for (int k = lane; k < NQ; k += 64) {
+    ctl->qhead[k] = s_head[k];
+    ctl->qtail[k] = s_tail[k];
+  }
+  const int ns = s_nseg;
+  for (int k = lane; k < ns; k += 64) ctl->seg[k] = s_seg[k];
+  int q = 0;
+#pragma unroll
+  for (int k = 0; k < NQ / 64; ++k) q += s_tail[lane + 64 * k] - s_head[lane + 64 * k];
+  q = wave_sum(q);
+  if (lane == 0) {
+    Batch nb = s_B;
+    if (specgo) {
+      spec_begin(ctl, nb, nb.L, s_qbase[nb.L] + s_head[nb.L], s_tail[nb.L] - s_head[nb.L]);
+      if (ctl->spec.fresh || ctl->spec.tstart == 0) {  // flood start, or after a cooldown: judge anew
+        ctl->spec.fresh = 0;
+        ctl->spec.accg = 0;
+        ctl->spec.tstart = (long long)__builtin_amdgcn_s_memrealtime();
+        ctl->spec.tspec = ctl->spec.pspec = 0;
+        ctl->spec.pstart = ctl->pops + cnt[0];  // this launch's pops, added below
+      }
+      ctl->spec.on = 1;
+      ctl->spec.block = 0;
+    }
+    ctl->bat = nb;
+    ctl->wcap = 0;
+    ctl->spec.cool = s_specool;
+    ctl->cut = NONE;
+    ctl->segcut = NONE;
+    ctl->minpush = NQ;
+    ctl->remaining = q;
+    ctl->batches += cnt[3];
+    ctl->pops += cnt[0];
+    ctl->items += cnt[1];
+    ctl->pushes += cnt[2];
+    ctl->lpops += cnt[0];
+    ctl->lpushes += cnt[2];
+    ctl->ser_go = 0;
+    if (s_err) ctl->error |= s_err;
+    if (s_B.n == 0 && !s_err) ctl->done = 1;
+    if (ws.diag) {
+      atomicAdd(&ws.diag[19], (unsigned long long)cnt[0]);
+      atomicAdd(&ws.diag[20], __builtin_amdgcn_s_memrealtime() - t0);
+    }
   }
 }
 

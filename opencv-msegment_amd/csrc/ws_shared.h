@@ -202,7 +202,9 @@ struct Ctl {
   int spec_want;     // the serial regime was entered while the speculative engine was enabled but
                      // its workspace not yet allocated (Ws.spec_lazy): the host allocates it
   unsigned hold;     // epoch of a decided batch k_commit_fast declined (k_resolve must not re-run it)
-  int pad3;
+  int ser_go;        // k_scan stopped at serial pops for k_serial_one, queued right after it
+  int ser_seen;      // the flood has reached the serial regime (the host then queues k_serial_one)
+  int pad4;
   // k_commit_fast: sub-round blocks done reading, by blockIdx % 8 (zeroed after): 480 atomics per
   // launch and the finalizer's polls, one 128-B line per counter (atomics on one line serialise at
   // the L2: with all 8 counters on one line k_commit_fast took 14.8 us per launch, round 4)
