@@ -585,8 +585,9 @@ int flood_loop(msg_ctx* c, FloodRun& fr) {
         LAUNCH(c, KID_RESOLVE, st, k_resolve<false>, dim3(gres), dim3(RBS), 0, ws);
       }
       // + small batches; in the serial regime k_serial_one pops what k_scan's loop hands it
-      LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws, (ser_it && !spec_it) ? 1 : 0);
-      if (ser_it && !spec_it) LAUNCH(c, KID_SERIAL_MULTI, st, k_serial_one, dim3(1), dim3(64), 0, ws);
+      // (in a speculative iteration too: a cooldown's serial pops start in its k_scan)
+      LAUNCH(c, KID_SCAN, st, k_scan, dim3(1), dim3(1024), 0, ws, ser_it ? 1 : 0);
+      if (ser_it) LAUNCH(c, KID_SERIAL_MULTI, st, k_serial_one, dim3(1), dim3(64), 0, ws);
       LAUNCH(c, KID_SCATTER, st, k_scatter, dim3(gsc), dim3(1024), 0, ws, it);
     }
     HIPCHK(c, hipGetLastError());
