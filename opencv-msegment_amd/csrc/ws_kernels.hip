@@ -2230,6 +2230,10 @@ __device__ __forceinline__ bool attempt_item_slots(const Item& it, const int (&v
 constexpr int TINY_MAX = 64;
 constexpr int SERIAL_RUN = 4096;    // serial pops: clean pops after which batches pay again
 constexpr int SERIAL_SWITCH = 16;   // a tiny batch cut before this many items -> serial pops
+// k_serial_one's (a single flood's serial phases after its first): 4096 -> 16384 took the NC
+// pipeline at 4096^2 1.97 -> 2.18 Mpx/s and album.jpg 969 -> 930 ms, the colour pipeline 3.34 -> 3.24
+// (profiles/r06sp_ab_serial_run.log)
+constexpr int SERIAL_RUN_ONE = 16384;
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -2955,7 +2959,7 @@ __global__ __launch_bounds__(64) void k_serial_one(Ws ws) {
   long long cnt[4] = {0, 0, 0, 0};
   const unsigned long long t0 = ws.diag ? __builtin_amdgcn_s_memrealtime() : 0;
   serial_loop_lanes<false>(ws, &s_B, s_seg, s_qbase, s_head, s_tail, &s_wcap, &s_err, &s_nseg, &s_n, &s_ser, cnt,
-                           specblk > 0 ? specblk : 0, specblk >= 0 ? &s_specool : nullptr, SERIAL_RUN);
+                           specblk > 0 ? specblk : 0, specblk >= 0 ? &s_specool : nullptr, SERIAL_RUN_ONE);
   wave_sync();
   // the cascade that stopped the speculative engine is done, or its cooldown is over: hand the
   // regime back to it (as k_scan's small-batch loop does)
